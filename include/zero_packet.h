@@ -1,0 +1,210 @@
+/*
+ * zero_packet.h — C ABI of the MI355X-native batched PacketParser::parse.
+ *
+ * This is the drop-in boundary for zero-packet's parse path
+ * (/root/reference/src/packet/parser.rs:53). The reference has no FFI of its
+ * own; its boundary is the Rust API
+ *
+ *     pub fn PacketParser::parse(bytes: &'a [u8]) -> Result<PacketParser<'a>, &'static str>
+ *
+ * whose result is nine `Option<Reader>` fields (parser.rs:22-32). Every
+ * reader is a sub-slice `&frame[start..]` that runs to the end of the frame,
+ * so a parsed packet is fully described by header START OFFSETS. One
+ * zp_record per frame carries those offsets plus presence bits, so a caller
+ * (C++ facade include/zero_packet.hpp, the Rust shim in INTEGRATION.md) can
+ * rebuild every reader without re-parsing.
+ *
+ * Plain pointers and sizes only; no torch types. Device pointers are HIP
+ * device memory; hipStream_t is passed as void*.
+ */
+#ifndef ZERO_PACKET_H
+#define ZERO_PACKET_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ZP_ABI_VERSION 1
+
+/* ------------------------------------------------------------------------- */
+/* Per-packet parse error codes. One code per DISTINCT reference error string */
+/* (identical strings collapse: icmpv4.rs:94 == icmpv6.rs:91). zp_err_str()   */
+/* returns the exact reference string. Codes marked (unreachable) cannot be   */
+/* produced by parse() because an earlier check subsumes them; they exist so  */
+/* the per-reader views can report them.                                      */
+/* ------------------------------------------------------------------------- */
+typedef enum zp_err {
+    ZP_OK = 0,
+    ZP_ERR_ETH_FRAME_TOO_SHORT = 1,   /* parser.rs:160                          */
+    ZP_ERR_ETH_SLICE_TOO_SHORT = 2,   /* ethernet.rs:143 (unreachable)          */
+    ZP_ERR_ETH_VLAN_TOO_SHORT = 3,    /* ethernet.rs:160 (unreachable)          */
+    ZP_ERR_ETH_QINQ_TOO_SHORT = 4,    /* ethernet.rs:167 (unreachable)          */
+    ZP_ERR_ETH_INVALID_QINQ = 5,      /* ethernet.rs:172                        */
+    ZP_ERR_ARP_TOO_SHORT = 6,         /* arp.rs:132 (unreachable)               */
+    ZP_ERR_ARP_INVALID_OPER = 7,      /* parser.rs:176                          */
+    ZP_ERR_IPV4_TOO_SHORT = 8,        /* ipv4.rs:140 (encapsulated levels only) */
+    ZP_ERR_IPV4_VERSION = 9,          /* parser.rs:192                          */
+    ZP_ERR_IPV4_IHL_TOO_SHORT = 10,   /* parser.rs:196                          */
+    ZP_ERR_IPV4_HDR_TOO_LONG = 11,    /* parser.rs:200                          */
+    ZP_ERR_IPV4_TOTAL_LENGTH = 12,    /* parser.rs:204                          */
+    ZP_ERR_IPV4_CHECKSUM = 13,        /* parser.rs:208                          */
+    ZP_ERR_IPV4_HDR_EXCEEDS = 14,     /* ipv4.rs:240,254 (unreachable)          */
+    ZP_ERR_IPV6_TOO_SHORT = 15,       /* ipv6.rs:149 (encapsulated levels only) */
+    ZP_ERR_IPV6_VERSION = 16,         /* parser.rs:226                          */
+    ZP_ERR_EXT_HBH_NOT_FIRST = 17,    /* headers.rs:99-101                      */
+    ZP_ERR_EXT_OPTIONS_TOO_SHORT = 18,/* options.rs:85                          */
+    ZP_ERR_EXT_OPTIONS_EXCEEDS = 19,  /* options.rs:149                         */
+    ZP_ERR_EXT_ROUTING_TOO_SHORT = 20,/* routing.rs:109                         */
+    ZP_ERR_EXT_ROUTING_EXCEEDS = 21,  /* routing.rs:190                         */
+    ZP_ERR_EXT_FRAGMENT_TOO_SHORT = 22,/* fragment.rs:99                        */
+    ZP_ERR_EXT_AUTH_TOO_SHORT = 23,   /* authentication.rs:107                  */
+    ZP_ERR_EXT_AUTH_EXCEEDS = 24,     /* authentication.rs:195                  */
+    ZP_ERR_TCP_TOO_SHORT = 25,        /* tcp.rs:143                             */
+    ZP_ERR_TCP_DATA_OFFSET = 26,      /* parser.rs:242                          */
+    ZP_ERR_TCP_FLAGS = 27,            /* parser.rs:246                          */
+    ZP_ERR_UDP_TOO_SHORT = 28,        /* udp.rs:105                             */
+    ZP_ERR_UDP_LENGTH = 29,           /* parser.rs:262                          */
+    ZP_ERR_ICMP_TOO_SHORT = 30,       /* icmpv4.rs:94 == icmpv6.rs:91           */
+    ZP_ERR_ICMPV4_TYPE = 31,          /* parser.rs:278                          */
+    ZP_ERR_ICMPV4_CODE = 32,          /* parser.rs:282                          */
+    ZP_ERR_ICMPV6_TYPE = 33,          /* parser.rs:298                          */
+    ZP_ERR_IPV4_L4_CHECKSUM = 34,     /* parser.rs:329                          */
+    ZP_ERR_IPV6_L4_CHECKSUM = 35,     /* parser.rs:357                          */
+    ZP_ERR_COUNT = 36
+} zp_err;
+
+/* ------------------------------------------------------------------------- */
+/* Presence bits of zp_record.flags: the nine Option fields of PacketParser   */
+/* (parser.rs:23-31) plus the IpInIp tag (misc.rs:6-9) and the two            */
+/* Option<ExtensionHeaders> (ipv6.rs:140) with their six Option readers each  */
+/* (headers.rs:20-25).                                                        */
+/* ------------------------------------------------------------------------- */
+#define ZP_F_ETHERNET      (1u << 0)
+#define ZP_F_ARP           (1u << 1)
+#define ZP_F_IPV4          (1u << 2)   /* outermost IPv4 (from Ethernet)        */
+#define ZP_F_IPV6          (1u << 3)   /* outermost IPv6 (from Ethernet)        */
+#define ZP_F_IP_IN_IP      (1u << 4)   /* first encapsulated IP header          */
+#define ZP_F_IP_IN_IP_V6   (1u << 5)   /* ... and it is IpInIp::Ipv6            */
+#define ZP_F_TCP           (1u << 6)
+#define ZP_F_UDP           (1u << 7)
+#define ZP_F_ICMPV4        (1u << 8)
+#define ZP_F_ICMPV6        (1u << 9)
+#define ZP_F_EXT           (1u << 10)  /* ipv6.extension_headers.is_some()      */
+#define ZP_F_INNER_EXT     (1u << 11)  /* ip_in_ip IPv6 extension_headers Some  */
+/* Extension header slots, in ExtensionHeaders field order (headers.rs:20-25). */
+#define ZP_EXT_HBH   0
+#define ZP_EXT_RT    1
+#define ZP_EXT_FRAG  2
+#define ZP_EXT_AH    3
+#define ZP_EXT_DST1  4
+#define ZP_EXT_DST2  5
+#define ZP_EXT_SLOTS 6
+#define ZP_F_EXT_SLOT(k)       (1u << (12 + (k)))  /* outer set, k in [0,6) */
+#define ZP_F_INNER_EXT_SLOT(k) (1u << (18 + (k)))  /* inner set             */
+
+/*
+ * One parse result, 32 bytes. All offsets are FRAME offsets (bytes from the
+ * first byte of the frame) unless stated. When err != ZP_OK the reference
+ * returns Err and no PacketParser exists: the record is then all zero except
+ * `err`.
+ *
+ *  - ethernet/arp/ipv4/ipv6 start at offsets 0 / eth_len / eth_len / eth_len.
+ *  - ext_off[k] is relative to the outer IPv6 payload (frame offset
+ *    eth_len + 40 + ext_off[k]); ext_len = IPv6Reader::extension_headers_len
+ *    (ipv6.rs:141); final_nh = IPv6Reader::final_next_header() (ipv6.rs:219).
+ *  - inner_off is the ip_in_ip header; its IPv6 extension offsets (relative to
+ *    inner_off + 40) go to the optional zp_ext_offsets side array.
+ *  - l4_off is the start of the single tcp/udp/icmpv4/icmpv6 reader.
+ */
+typedef struct zp_record {
+    uint32_t flags;
+    uint8_t  err;
+    uint8_t  eth_len;        /* 14, 18 or 22 (ethernet.rs:155-179)        */
+    uint8_t  final_nh;       /* outer IPv6 final next header               */
+    uint8_t  inner_final_nh; /* ip_in_ip IPv6 final next header            */
+    uint32_t inner_off;
+    uint32_t l4_off;
+    uint16_t ext_len;
+    uint16_t ext_off[ZP_EXT_SLOTS];
+    uint16_t inner_ext_len;
+} zp_record;
+
+/* Extension offsets of the ip_in_ip IPv6 header (written only when
+ * flags & ZP_F_INNER_EXT; relative to the inner IPv6 payload). */
+typedef struct zp_ext_offsets {
+    uint16_t off[ZP_EXT_SLOTS];
+} zp_ext_offsets;
+
+/* ------------------------------------------------------------------------- */
+/* Library info                                                              */
+/* ------------------------------------------------------------------------- */
+/* Returns ZP_ABI_VERSION. */
+int zp_abi_version(void);
+/* Exact reference error string for a zp_err code ("" for ZP_OK, NULL if out
+ * of range). Replaces the `&'static str` of Result (parser.rs:53). */
+const char* zp_err_str(int code);
+/* Last HIP error string seen by this library on the calling thread. */
+const char* zp_last_error(void);
+
+/* ------------------------------------------------------------------------- */
+/* Batch parse — the hot path.                                                */
+/* Replaces a loop of PacketParser::parse(&arena[off[i]..off[i]+len[i]])      */
+/* (parser.rs:53) over n frames.                                              */
+/* ------------------------------------------------------------------------- */
+/*
+ * Device-resident batch parse. All pointers are device memory on the current
+ * HIP device; the call only enqueues work on `stream` (a hipStream_t, NULL =
+ * default stream) and returns. Frames may lie anywhere in `arena` (gaps,
+ * overlaps and any order are allowed); the fast path is taken for the common
+ * packed, increasing layout. `inner_ext` may be NULL. Returns 0 on success or
+ * a negative value if the launch failed (see zp_last_error()).
+ */
+int zp_parse_batch_device(const uint8_t* arena, const uint64_t* offs,
+                          const uint32_t* lens, uint64_t n,
+                          zp_record* records, zp_ext_offsets* inner_ext,
+                          void* stream);
+
+/* Host-buffer convenience path: the frames, descriptors and outputs live in
+ * host memory (a NIC ring / raw socket buffer). Stages through pinned buffers
+ * and overlaps H2D copy, parse and D2H copy in chunks on `ctx`'s streams.
+ * Synchronous. Returns 0 on success, negative on HIP failure. */
+typedef struct zp_ctx zp_ctx;
+zp_ctx* zp_ctx_create(int device, uint64_t chunk_bytes);
+void    zp_ctx_destroy(zp_ctx* ctx);
+int zp_parse_batch_host(zp_ctx* ctx, const uint8_t* arena, uint64_t arena_bytes,
+                        const uint64_t* offs, const uint32_t* lens, uint64_t n,
+                        zp_record* records, zp_ext_offsets* inner_ext);
+/* One frame through the GPU path (PacketParser::parse equivalent).
+ * Returns the zp_err code (>= 0) or a negative value on HIP failure. */
+int zp_parse_one(zp_ctx* ctx, const uint8_t* frame, uint64_t len,
+                 zp_record* record, zp_ext_offsets* inner_ext);
+
+/* ------------------------------------------------------------------------- */
+/* Synthetic batch generator (BASELINE.json configs 1-5), built from the      */
+/* builder's checksum-fill semantics (builder.rs:473-474,515-516,553,592-593).*/
+/* Deterministic per packet: packet i depends only on (config, seed, i).      */
+/* ------------------------------------------------------------------------- */
+#define ZP_CFG_C1_ETH_IPV4_UDP_64 1  /* == C2 layout, CPU plumbing            */
+#define ZP_CFG_C2_ETH_IPV4_UDP_64 2
+#define ZP_CFG_C3_IPV4_MIX        3
+#define ZP_CFG_C4_IPV6_EXT_VLAN   4
+#define ZP_CFG_C5_IMIX_IPINIP     5
+#define ZP_GEN_SEED_DEFAULT 0x5EED2025ull
+
+/* Frame length of packet `first + i`, i in [0, n), into d_lens (device). */
+int zp_gen_lengths_device(int config, uint64_t seed, uint64_t first, uint64_t n,
+                          uint32_t* lens, void* stream);
+/* Writes frame `first + i` at arena + offs[i] (offs/lens device arrays as
+ * produced by zp_gen_lengths_device + an exclusive scan). */
+int zp_gen_frames_device(int config, uint64_t seed, uint64_t first, uint64_t n,
+                         uint8_t* arena, const uint64_t* offs,
+                         const uint32_t* lens, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ZERO_PACKET_H */

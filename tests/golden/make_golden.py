@@ -1,0 +1,242 @@
+"""Generates tests/golden/parse_golden.json from the reference's own tests.
+
+Run once in the build container (the reference is mounted read-only at
+/root/reference there; it is NOT present on the GPU box, so tests only read
+the committed JSON):
+
+    python tests/golden/make_golden.py /root/reference
+
+What it writes, per fixture:
+  - `bytes`: the frame, hex. For parser.rs tests and the builder `should_be` /
+    `assert_eq!(packet, [...])` vectors this is the byte-array literal of the
+    reference test, extracted from the source at the cited line. For the
+    builder round-trip tests (which build their frame at run time) it is the
+    output of tests/pybuilder.py for the same builder calls.
+  - `expect`: the outcome the reference test asserts (is_ok / is_err, which
+    Option fields are Some / None, asserted field values), transcribed from
+    the cited assert lines. `err` is only given where the test asserts
+    is_err (or, for builder vectors the tests never parse, marked
+    "derived": the first failing check of parser.rs for that frame).
+Also the checksum.rs:75-133 known-answer tests.
+"""
+import json
+import os
+import re
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+from pybuilder import Builder  # noqa: E402
+
+
+def array_after(lines, lineno):
+    """Integer array literal starting at or after 1-based `lineno`."""
+    text = []
+    i = lineno - 1
+    depth = 0
+    started = False
+    while i < len(lines):
+        line = re.sub(r"//.*", "", lines[i])
+        for ch in line:
+            if ch == "[":
+                depth += 1
+                started = True
+                text.append(ch)
+            elif ch == "]" and started:
+                depth -= 1
+                text.append(ch)
+                if depth == 0:
+                    body = "".join(text)
+                    nums = re.findall(r"0x[0-9a-fA-F]+|\d+", body)
+                    return [int(x, 0) for x in nums], i + 1
+            elif started:
+                text.append(ch)
+        i += 1
+    raise ValueError(f"no array after line {lineno}")
+
+
+def main(ref):
+    parser_rs = open(os.path.join(ref, "src/packet/parser.rs")).read().splitlines()
+    builder_rs = open(os.path.join(ref, "src/packet/builder.rs")).read().splitlines()
+
+    def pr(line):
+        arr, end = array_after(parser_rs, line)
+        return arr, f"src/packet/parser.rs:{line}-{end}"
+
+    def br(line):
+        arr, end = array_after(builder_rs, line)
+        return arr, f"src/packet/builder.rs:{line}-{end}"
+
+    L4 = ["tcp", "udp", "icmpv4", "icmpv6"]
+    fixtures = []
+
+    def add(name, arr, src, expect, asserts):
+        fixtures.append({"name": name, "source": src, "asserts": asserts,
+                         "bytes": bytes(arr).hex(), "expect": expect})
+
+    # ---- parser.rs tests -------------------------------------------------
+    a, s = pr(371)
+    add("parse_frame_too_short", a, s, {"ok": False, "err": "ETH_FRAME_TOO_SHORT"},
+        "src/packet/parser.rs:380 (is_err)")
+    a, s = pr(387)
+    add("vlan_tagged_frame", a, s, {
+        "ok": True, "some": ["ethernet", "ipv4", "udp"], "none": ["icmpv4", "arp", "tcp"],
+        "fields": {"ethernet.vlan_tag": [0x8100, 100], "ethernet.double_vlan_tag": None,
+                   "ethernet.ethertype": 0x0800}}, "src/packet/parser.rs:415-442")
+    a, s = pr(447)
+    add("double_vlan_tagged_frame", a, s, {
+        "ok": True, "some": ["ethernet", "ipv4", "udp"], "none": ["icmpv4", "arp", "tcp"],
+        "fields": {"ethernet.vlan_tag": None,
+                   "ethernet.double_vlan_tag": [[0x88A8, 200], [0x8100, 100]],
+                   "ethernet.ethertype": 0x0800}}, "src/packet/parser.rs:473-505")
+    a, s = pr(511)
+    add("icmpv4_echo_response", a, s, {
+        "ok": True, "some": ["ethernet", "ipv4", "icmpv4"], "none": ["arp", "tcp", "udp"],
+        "fields": {"ethernet.ethertype": 0x0800, "ipv4.protocol": 1, "ipv4.checksum": 0xfa30,
+                   "icmpv4.icmp_type": 0, "icmpv4.icmp_code": 0, "icmpv4.checksum": 0x45da}},
+        "src/packet/parser.rs:522-549")
+    a, s = pr(555)
+    add("ipv6_icmpv6", a, s, {
+        "ok": True, "some": ["ethernet", "ipv6", "icmpv6"],
+        "none": ["icmpv4", "arp", "tcp", "udp"],
+        "fields": {"ethernet.ethertype": 34525, "ipv6.next_header": 58,
+                   "icmpv6.icmp_type": 135, "icmpv6.icmp_code": 0}},
+        "src/packet/parser.rs:565-594")
+    a, s = pr(600)
+    add("ipv6_udp_payload", a, s, {
+        "ok": True, "some": ["ethernet", "ipv6", "udp"],
+        "none": ["icmpv4", "icmpv6", "arp", "tcp"],
+        "fields": {"udp.payload": [0x07, 0x03, 0x00, 0x00, 0xf9, 0xc8, 0xe7, 0x36,
+                                   0xef, 0x5d, 0x0a, 0x00]}},
+        "src/packet/parser.rs:609-636")
+    a, s = pr(642)
+    add("ipv6_routing_extension_header", a, s, {
+        "ok": True, "some": ["ethernet", "ipv6", "tcp"], "none": ["icmpv4", "icmpv6", "arp", "udp"],
+        "ext_some": ["routing"]}, "src/packet/parser.rs:657-686")
+    a, s = pr(692)
+    add("ipv6_hop_by_hop_options", a, s, {
+        "ok": True, "some": ["ethernet", "ipv6", "tcp"], "none": ["icmpv4", "icmpv6", "arp", "udp"],
+        "ext_some": ["hop_by_hop"]}, "src/packet/parser.rs:701-731")
+    a, s = pr(737)
+    add("ipv6_destination_options", a, s, {
+        "ok": True, "some": ["ethernet", "ipv6", "tcp"], "none": ["icmpv4", "icmpv6", "arp", "udp"],
+        "ext_some": ["destination_1st"]}, "src/packet/parser.rs:746-776")
+    a, s = pr(782)
+    add("fragment_header_icmpv6", a, s, {"ok": True}, "src/packet/parser.rs:802-804")
+    a, s = pr(807)
+    add("authentication_header", a, s, {"ok": True}, "src/packet/parser.rs:820-823")
+    a, s = pr(830)
+    add("extension_headers_chained", a, s, {
+        "ok": True, "some": ["ethernet", "ipv6"],
+        "none": ["icmpv4", "icmpv6", "arp", "udp", "tcp"],
+        "ext_some": ["hop_by_hop", "destination_1st"]}, "src/packet/parser.rs:854-885")
+    a, s = pr(891)
+    add("ipv6_in_ipv6_with_extension_header", a, s, {"ok": True},
+        "src/packet/parser.rs:909-913")
+    a, s = pr(918)
+    add("ipv6_in_ipv4", a, s, {"ok": True}, "src/packet/parser.rs:932-936")
+    a, s = pr(941)
+    add("ipv4_in_ipv4", a, s, {"ok": True}, "src/packet/parser.rs:953-957")
+
+    # ---- builder.rs exact vectors -----------------------------------------
+    builder_vectors = []
+    for name, line in [("arp_in_ethernet", 1052), ("tcp_in_ipv4_in_ethernet", 1097),
+                       ("udp_in_ipv4_in_ethernet", 1161), ("icmpv4_in_ipv4_in_ethernet", 1212),
+                       ("build_parse_ipv6", 1290)]:
+        a, s = br(line)
+        builder_vectors.append({"name": name, "source": s, "bytes": bytes(a).hex()})
+
+    for v in builder_vectors:
+        a = list(bytes.fromhex(v["bytes"]))
+        if v["name"] == "build_parse_ipv6":
+            add("build_parse_ipv6", a, v["source"], {
+                "ok": True, "some": ["ethernet", "ipv6", "udp"], "none": ["arp", "icmpv4", "tcp"]},
+                "src/packet/builder.rs:1299-1317")
+        elif v["name"] == "icmpv4_in_ipv4_in_ethernet":
+            add(v["name"], a, v["source"], {"ok": False, "err": "IPV4_TOTAL_LENGTH",
+                                            "derived": True},
+                "derived: total_length 12345 != 50 (parser.rs:203)")
+        else:
+            add(v["name"], a, v["source"], {"ok": False, "err": "ETH_FRAME_TOO_SHORT",
+                                            "derived": True},
+                "derived: frame shorter than 64 B (parser.rs:159)")
+
+    # ---- builder.rs round trips (frames from tests/pybuilder.py) ----------
+    m1 = [0x34, 0x97, 0xf6, 0x94, 0x02, 0x0f]
+    m2 = [0x04, 0xb4, 0xfe, 0x9a, 0x81, 0xc7]
+    ip1, ip2 = [192, 168, 1, 1], [192, 168, 1, 2]
+    pay = list(range(1, 11))
+    f = (Builder(64).ethernet([1, 2, 3, 4, 5, 6], [7, 8, 9, 10, 11, 12], 0x0800)
+         .ipv4(4, 5, 0, 0, 50, 0, 0, 0, 64, 17, ip1, ip2)
+         .udp(ip1, 12345, ip2, 54321, 30, pay).build())
+    add("write_payload", list(f), "src/packet/builder.rs:920-993 (built by tests/pybuilder.py)", {
+        "ok": True, "some": ["udp"], "fields": {"udp.payload": pay + [0] * 12}},
+        "src/packet/builder.rs:974-992")
+    f = (Builder(64).ethernet_qinq(m1, m2, 2048, 200, 100)
+         .ipv4(4, 5, 99, 123, 42, 54321, 99, 12345, 123, 17, ip1, ip2)
+         .udp(ip1, 99, ip2, 11, 22).build())
+    add("build_parse_qinq", list(f), "src/packet/builder.rs:1320-1390 (built by tests/pybuilder.py)", {
+        "ok": True, "some": ["ethernet", "ipv4", "udp"], "none": ["arp", "icmpv4", "tcp"],
+        "fields": {"ethernet.vlan_tag": None,
+                   "ethernet.double_vlan_tag": [[0x88A8, 200], [0x8100, 100]],
+                   "ethernet.src_mac": m1, "ethernet.dest_mac": m2,
+                   "ethernet.ethertype": 2048}}, "src/packet/builder.rs:1357-1389")
+    s6 = [0x20, 0x01, 0x0d, 0xb8, 0x85, 0xa3, 0, 0, 0, 0, 0x8a, 0x2e, 0x03, 0x70, 0x73, 0x34]
+    d6 = [0xfe, 0x80, 0, 0, 0, 0, 0, 0, 0x02, 0x02, 0xb3, 0xff, 0xfe, 0x1e, 0x83, 0x29]
+    f = (Builder(70).ethernet_qinq(m1, m2, 34525, 200, 100)
+         .ipv6(6, 5, 4, 3, 58, 255, s6, d6).icmpv6(s6, d6, 128, 0).build())
+    add("build_parse_qinq_icmpv6", list(f),
+        "src/packet/builder.rs:1393-1448 (built by tests/pybuilder.py)", {
+            "ok": True, "some": ["ethernet", "ipv6", "icmpv6"],
+            "none": ["arp", "udp", "tcp", "icmpv4"]}, "src/packet/builder.rs:1429-1447")
+    f = (Builder(300).ethernet_qinq(m1, m2, 34525, 200, 100)
+         .ipv6(6, 5, 4, 3, 0, 255, [0] * 16, [0] * 16)
+         .hop_by_hop(60, 1, [1] * 8)
+         .destination_options1(43, 1, [1] * 8)
+         .routing_header(44, 1, 2, 3, [2] * 8)
+         .fragment_header(51, 255, True, 0x04050607)
+         .authentication_header(60, 2, 305419896, 2271560481, [1] * 8)
+         .destination_options2(4, 1, [1] * 8)
+         .ipv4(4, 5, 0, 0, 150, 0, 0, 0, 64, 6, ip1, ip2)
+         .tcp(ip1, 99, ip2, 11, 123, 321, 11, 99, 99, 4321, 1234, pay).build())
+    add("build_parse_very_complex_packet", list(f),
+        "src/packet/builder.rs:1450-1556 (built by tests/pybuilder.py)", {
+            "ok": True, "some": ["ethernet", "ipv6", "ip_in_ip", "tcp"],
+            "none": ["arp", "udp", "icmpv4", "icmpv6"],
+            "ext_some": ["hop_by_hop", "destination_1st", "routing", "fragment",
+                         "auth_header", "destination_2nd"],
+            "ip_in_ip": "ipv4"}, "src/packet/builder.rs:1511-1555")
+
+    # ---- checksum.rs KATs --------------------------------------------------
+    cs = open(os.path.join(ref, "src/network/checksum.rs")).read().splitlines()
+
+    def ca(line):
+        arr, end = array_after(cs, line)
+        return arr, f"src/network/checksum.rs:{line}-{end}"
+
+    kats = [
+        {"data": [0] * 8, "acc": 0, "checksum": 65535, "source": "src/network/checksum.rs:76-80"},
+        {"data": [255] * 8, "acc": 0, "checksum": 0, "source": "src/network/checksum.rs:83-87"},
+    ]
+    for line, want, lo, hi in [(91, 0xd374, 90, 97), (101, 0xb861, 100, 107), (111, 0x210e, 110, 114)]:
+        a, _ = ca(line)
+        kats.append({"data": a, "acc": 0, "checksum": want,
+                     "source": f"src/network/checksum.rs:{lo}-{hi}"})
+    a, _ = ca(118)
+    kats.append({"data": a, "acc": 0, "checksum": 0, "verify": True,
+                 "source": "src/network/checksum.rs:117-123"})
+    pseudo = {"src": [192, 168, 0, 1], "dst": [192, 168, 0, 199], "protocol": 6, "length": 20,
+              "sum": 98866, "source": "src/network/checksum.rs:126-133"}
+
+    out = {"generated_by": "tests/golden/make_golden.py",
+           "reference": "J-Schoepplenberg/zero-packet 0.1.0",
+           "fixtures": fixtures, "builder_vectors": builder_vectors,
+           "checksum_kats": kats, "pseudo_header_kat": pseudo}
+    with open(os.path.join(HERE, "parse_golden.json"), "w") as fh:
+        json.dump(out, fh, indent=1)
+    print(f"wrote {len(fixtures)} fixtures, {len(builder_vectors)} builder vectors, "
+          f"{len(kats)} checksum KATs")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "/root/reference")

@@ -1,0 +1,76 @@
+"""ctypes wrapper of the CPU oracle (oracle/libzp_oracle.so) — the checker.
+
+Test infrastructure: only tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg use it. Built by `make -C oracle` (also by build()).
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "oracle", "libzp_oracle.so")
+_lib = None
+
+RECORD_DTYPE = np.dtype([
+    ("flags", "<u4"), ("err", "u1"), ("eth_len", "u1"), ("final_nh", "u1"),
+    ("inner_final_nh", "u1"), ("inner_off", "<u4"), ("l4_off", "<u4"),
+    ("ext_len", "<u2"), ("ext_off", "<u2", (6,)), ("inner_ext_len", "<u2"),
+])
+EXT_DTYPE = np.dtype([("off", "<u2", (6,))])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+        l = ctypes.CDLL(LIB)
+        vp, u64, i32, sz = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_size_t
+        l.zpo_parse.restype = i32
+        l.zpo_parse.argtypes = [vp, sz, vp, vp]
+        l.zpo_parse_batch.restype = i32
+        l.zpo_parse_batch.argtypes = [vp, vp, vp, u64, vp, vp, i32]
+        l.zpo_internet_checksum.restype = ctypes.c_uint16
+        l.zpo_internet_checksum.argtypes = [vp, sz, ctypes.c_uint32]
+        l.zpo_pseudo_header.restype = ctypes.c_uint32
+        l.zpo_pseudo_header.argtypes = [vp, vp, sz, ctypes.c_uint8, sz]
+        _lib = l
+    return _lib
+
+
+def parse_one(frame):
+    """-> (err, record[RECORD_DTYPE], inner_ext[EXT_DTYPE])"""
+    frame = bytes(frame)
+    buf = ctypes.create_string_buffer(frame, max(len(frame), 1))
+    rec = np.zeros(1, RECORD_DTYPE)
+    ext = np.zeros(1, EXT_DTYPE)
+    err = lib().zpo_parse(ctypes.addressof(buf), len(frame), rec.ctypes.data, ext.ctypes.data)
+    return err, rec[0], ext[0]
+
+
+def parse_batch(arena, offs, lens, nthreads=0):
+    arena = np.ascontiguousarray(arena, dtype=np.uint8)
+    offs = np.ascontiguousarray(offs).astype(np.uint64, copy=False)
+    lens = np.ascontiguousarray(lens).astype(np.uint32, copy=False)
+    n = len(offs)
+    rec = np.zeros(n, RECORD_DTYPE)
+    ext = np.zeros(n, EXT_DTYPE)
+    if n:
+        lib().zpo_parse_batch(arena.ctypes.data, offs.ctypes.data, lens.ctypes.data, n,
+                              rec.ctypes.data, ext.ctypes.data, nthreads)
+    return rec, ext
+
+
+def internet_checksum(data, acc=0):
+    data = bytes(data)
+    buf = ctypes.create_string_buffer(data, max(len(data), 1))
+    return lib().zpo_internet_checksum(ctypes.addressof(buf), len(data), acc)
+
+
+def pseudo_header(src, dst, protocol, length):
+    s = ctypes.create_string_buffer(bytes(src))
+    d = ctypes.create_string_buffer(bytes(dst))
+    return lib().zpo_pseudo_header(ctypes.addressof(s), ctypes.addressof(d), len(src),
+                                   protocol, length)

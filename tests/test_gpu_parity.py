@@ -1,0 +1,278 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle.
+
+Bit-exact on every record byte (integer/byte work). Covers the reference's
+golden packets, all five synthetic configs, mutation fuzz, odd layouts
+(gaps, overlap, reverse order, odd base address), edge lengths, jumbo IPv6
+frames (exact u32-wrap checksum path), the host-buffer path, and full-size
+C3 properties.
+"""
+import ctypes
+import random
+
+import numpy as np
+import pytest
+
+import oracle as orc
+from test_oracle_fuzz import mutate
+from test_oracle_golden import ERR, check_expect
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    return torch.device("cuda:0")
+
+
+def pack(frames, base_pad=0, gap=0):
+    """frames -> host (arena, offs, lens), frames back to back (plus gap)."""
+    offs, pos = [], base_pad
+    for f in frames:
+        offs.append(pos)
+        pos += len(f) + gap
+    arena = np.zeros(pos + 64, np.uint8)
+    for o, f in zip(offs, frames):
+        arena[o:o + len(f)] = np.frombuffer(bytes(f), np.uint8)
+    return arena, np.array(offs, np.uint64), np.array([len(f) for f in frames], np.uint32)
+
+
+def gpu_parse(zp, arena, offs, lens, base_shift=0):
+    d = dev()
+    a = torch.zeros(len(arena) + base_shift + 16, dtype=torch.uint8, device=d)
+    a[base_shift:base_shift + len(arena)] = torch.from_numpy(np.asarray(arena, np.uint8)).to(d)
+    o = torch.from_numpy(np.asarray(offs, np.int64) + base_shift).to(d)
+    l_ = torch.from_numpy(np.asarray(lens, np.uint32).astype(np.int32)).to(d)
+    r, e = zp.batch.parse_batch(a, o, l_)
+    torch.cuda.synchronize()
+    return zp.batch.records_to_numpy(r, e)
+
+
+def assert_same(got, got_ext, want, want_ext):
+    bad = np.nonzero(got.view(np.uint8).reshape(-1, 32).any(1) !=
+                     want.view(np.uint8).reshape(-1, 32).any(1))[0]
+    diff = np.nonzero((got.view(np.uint8).reshape(-1, 32) !=
+                       want.view(np.uint8).reshape(-1, 32)).any(1))[0]
+    assert len(diff) == 0, (f"{len(diff)} records differ; first {diff[:5]}",
+                            got[diff[:3]], want[diff[:3]], bad[:3])
+    m = (want["flags"] & (1 << 11)) != 0
+    assert got_ext[m].tobytes() == want_ext[m].tobytes()
+
+
+# ---- golden packets ------------------------------------------------------
+
+def test_golden_batch(zp, golden):
+    frames = [bytes.fromhex(fx["bytes"]) for fx in golden["fixtures"]]
+    for shift in (0, 1, 3, 7):
+        arena, offs, lens = pack(frames)
+        got, gext = gpu_parse(zp, arena, offs, lens, base_shift=shift)
+        want, wext = orc.parse_batch(arena, offs, lens)
+        assert_same(got, gext, want, wext)
+        for fx, f, r, e in zip(golden["fixtures"], frames, got, gext):
+            check_expect(zp, f, r, e, fx["expect"])
+
+
+def test_golden_parse_one(zp, golden):
+    """PacketParser.parse (zp_parse_one: host frame -> GPU -> record)."""
+    for fx in golden["fixtures"]:
+        f = bytes.fromhex(fx["bytes"])
+        if fx["expect"]["ok"]:
+            p = zp.PacketParser.parse(f)
+            assert p.ethernet is not None
+        else:
+            with pytest.raises(zp.ZeroPacketError) as ei:
+                zp.PacketParser.parse(f)
+            if "err" in fx["expect"]:
+                assert ei.value.code == ERR[fx["expect"]["err"]]
+
+
+# ---- synthetic configs ---------------------------------------------------
+
+@pytest.mark.parametrize("cfg,n", [("c1", 50000), ("c3", 40000), ("c4", 40000),
+                                   ("c5", 60000)])
+def test_synthetic_configs_exact(zp, cfg, n):
+    arena, offs, lens = zp.batch.generate(cfg, n, first=99991, device=dev())
+    r, e = zp.batch.parse_batch(arena, offs, lens)
+    torch.cuda.synchronize()
+    got, gext = zp.batch.records_to_numpy(r, e)
+    want, wext = orc.parse_batch(arena.cpu().numpy(), offs.cpu().numpy(), lens.cpu().numpy())
+    assert (want["err"] == 0).all()
+    assert_same(got, gext, want, wext)
+
+
+@pytest.mark.parametrize("cfg", ["c1", "c3", "c4", "c5"])
+def test_device_generator_matches_host(zp, cfg):
+    n = 3000
+    a, o, l_ = zp.batch.generate(cfg, n, first=5, device=dev())
+    ha, ho, hl = zp.batch.generate_host(cfg, n, first=5)
+    assert (l_.cpu().numpy().astype(np.uint32) == hl).all()
+    assert a.cpu().numpy()[:int(ho[-1] + hl[-1])].tobytes() == ha[:int(ho[-1] + hl[-1])].tobytes()
+
+
+# ---- fuzz & layouts -------------------------------------------------------
+
+def fuzz_frames(zp, golden, count, seed):
+    rng = random.Random(seed)
+    seeds = [bytes.fromhex(fx["bytes"]) for fx in golden["fixtures"]]
+    for cfg in ("c3", "c4", "c5"):
+        a, o, l_ = zp.batch.generate_host(cfg, 64, first=seed)
+        seeds += [a[x:x + y].tobytes() for x, y in zip(o, l_)]
+    out = []
+    for _ in range(count):
+        f = rng.choice(seeds)
+        for _ in range(rng.randint(0, 2)):
+            f = mutate(rng, f)
+        out.append(f)
+    return out
+
+
+def test_fuzz_gpu_vs_oracle(zp, golden):
+    frames = fuzz_frames(zp, golden, 60000, 7)
+    arena, offs, lens = pack(frames)
+    got, gext = gpu_parse(zp, arena, offs, lens, base_shift=5)
+    want, wext = orc.parse_batch(arena, offs, lens)
+    assert_same(got, gext, want, wext)
+    assert len(np.unique(want["err"])) >= 18
+
+
+@pytest.mark.parametrize("layout", ["shuffled", "gaps", "overlap", "reverse", "dup"])
+def test_layouts(zp, golden, layout):
+    frames = fuzz_frames(zp, golden, 5000, 11)
+    arena, offs, lens = pack(frames, base_pad=3, gap=(13 if layout == "gaps" else 0))
+    rng = np.random.default_rng(3)
+    if layout == "shuffled":
+        p = rng.permutation(len(offs))
+        offs, lens = offs[p], lens[p]
+    elif layout == "reverse":
+        offs, lens = offs[::-1].copy(), lens[::-1].copy()
+    elif layout == "overlap":
+        # frames that share bytes: a second view starting 7 bytes into each frame
+        offs = np.concatenate([offs, offs + 7]).astype(np.uint64)
+        lens = np.concatenate([lens, np.maximum(lens.astype(np.int64) - 7, 0)]).astype(np.uint32)
+    elif layout == "dup":
+        idx = rng.integers(0, len(offs), 8000)
+        offs, lens = offs[idx], lens[idx]
+    got, gext = gpu_parse(zp, arena, offs, lens)
+    want, wext = orc.parse_batch(arena, offs, lens)
+    assert_same(got, gext, want, wext)
+
+
+def test_edge_lengths_and_empty(zp):
+    d = dev()
+    # n == 0: no launch, no error
+    a = torch.zeros(64, dtype=torch.uint8, device=d)
+    r, e = zp.batch.parse_batch(a, torch.zeros(0, dtype=torch.int64, device=d),
+                                torch.zeros(0, dtype=torch.int32, device=d))
+    assert r.numel() == 0
+    # every length 0..200 of a valid frame, the last one ending at the arena end
+    ha, ho, hl = zp.batch.generate_host("c3", 1, first=42)
+    base = ha[int(ho[0]):int(ho[0] + hl[0])].tobytes()
+    frames = [base[:k] for k in range(0, min(len(base), 200) + 1)]
+    arena, offs, lens = pack(frames)
+    arena = arena[:int(offs[-1] + lens[-1])]            # tight arena end
+    got, gext = gpu_parse(zp, arena, offs, lens)
+    want, wext = orc.parse_batch(arena, offs, lens)
+    assert_same(got, gext, want, wext)
+
+
+def _jumbo_ipv6(total_len, rng, valid=True, proto=17):
+    """IPv6 UDP/ICMPv6 frame of total_len bytes (payload_length is never
+    checked by the parser, so frames > 64 KiB are legal input)."""
+    from pybuilder import internet_checksum, pseudo_header
+    f = bytearray(rng.integers(0, 256, total_len, dtype=np.uint8).tobytes())
+    f[12:14] = b"\x86\xdd"
+    f[14] = 0x60
+    f[20] = proto
+    seg = total_len - 54
+    if proto == 17:
+        f[54 + 4:54 + 6] = (seg & 0xFFFF).to_bytes(2, "big")
+        f[58:60] = b"\0\0"
+        c = internet_checksum(f[54:], pseudo_header(f[22:38], f[38:54], 17, seg))
+        f[60:62] = (c if valid else c ^ 0x1).to_bytes(2, "big")
+    else:
+        f[54] = 128
+        f[56:58] = b"\0\0"
+        c = internet_checksum(f[54:], pseudo_header(f[22:38], f[38:54], 58, seg))
+        f[56:58] = (c if valid else c ^ 0x1).to_bytes(2, "big")
+    return bytes(f)
+
+
+def test_jumbo_frames_exact_path(zp):
+    """Segments > 64 KiB take the exact E/O path (u32 wrap reproduced)."""
+    rng = np.random.default_rng(5)
+    frames = []
+    for L in (65535, 65600, 70001, 140000, 200003, 300000):
+        for proto in (17, 58):
+            frames.append(_jumbo_ipv6(L, rng, True, proto))
+            frames.append(_jumbo_ipv6(L, rng, False, proto))
+    arena, offs, lens = pack(frames)
+    got, gext = gpu_parse(zp, arena, offs, lens, base_shift=1)
+    want, wext = orc.parse_batch(arena, offs, lens)
+    assert_same(got, gext, want, wext)
+    # UDP length field wraps for > 64 KiB segments -> UDP_LENGTH; ICMPv6 hits the checksum
+    assert set(np.unique(want["err"])) >= {0, ERR["IPV6_L4_CHECKSUM"]}
+
+
+def test_all_zero_icmp_never_valid(zp):
+    """S == 0 (acc 0, all-zero ICMPv4 message) is invalid (checksum.rs:28)."""
+    from pybuilder import Builder
+    ip1, ip2 = [10, 0, 0, 1], [10, 0, 0, 2]
+    f = bytearray(Builder(98).ethernet([1] * 6, [2] * 6, 0x0800)
+                  .ipv4(4, 5, 0, 0, 84, 0, 0, 0, 64, 1, ip1, ip2).icmpv4(0, 0).build())
+    f[36:] = bytes(len(f) - 36)            # ICMP type 0 code 0 checksum 0, zero body
+    arena, offs, lens = pack([bytes(f)])
+    got, gext = gpu_parse(zp, arena, offs, lens)
+    want, wext = orc.parse_batch(arena, offs, lens)
+    assert want["err"][0] == ERR["IPV4_L4_CHECKSUM"]
+    assert_same(got, gext, want, wext)
+
+
+# ---- host-buffer path -------------------------------------------------------
+
+@pytest.mark.parametrize("pinned", [False, True])
+def test_host_path(zp, golden, pinned):
+    frames = fuzz_frames(zp, golden, 20000, 21)
+    arena, offs, lens = pack(frames)
+    if pinned:
+        t = torch.from_numpy(arena).pin_memory()
+        arena = t.numpy()
+    lib = zp._lib.hip()
+    ctx = lib.zp_ctx_create(0, 1 << 20)           # small chunks: many slots in flight
+    assert ctx
+    rec = np.zeros(len(offs), zp.records.RECORD_DTYPE)
+    ext = np.zeros(len(offs), zp.records.EXT_DTYPE)
+    rc = lib.zp_parse_batch_host(ctx, arena.ctypes.data, len(arena), offs.ctypes.data,
+                                 lens.ctypes.data, len(offs), rec.ctypes.data, ext.ctypes.data)
+    lib.zp_ctx_destroy(ctx)
+    assert rc == 0, lib.zp_last_error()
+    want, wext = orc.parse_batch(arena, offs, lens)
+    assert_same(rec, ext, want, wext)
+
+
+# ---- full-size C3 properties ----------------------------------------------
+
+def test_full_size_c3_properties(zp):
+    """BASELINE config 3 at full size (16M frames, ~13 GB): every frame
+    accepted, a 200k random sample byte-exact vs the oracle, idempotent
+    re-parse, and flipping one L4 byte per frame turns every record into the
+    checksum error."""
+    n = 16 * 1024 * 1024
+    arena, offs, lens = zp.batch.generate("c3", n, device=dev())
+    r1, e1 = zp.batch.parse_batch(arena, offs, lens)
+    err = r1[:, 4]
+    assert int((err != 0).sum()) == 0
+    r2, _ = zp.batch.parse_batch(arena, offs, lens)
+    assert torch.equal(r1, r2)
+    idx = torch.randint(0, n, (2000,), device=arena.device, generator=torch.Generator(
+        device=arena.device).manual_seed(1))
+    so, sl = offs[idx].cpu().numpy(), lens[idx].cpu().numpy()
+    frames = [arena[int(o):int(o) + int(l)].cpu().numpy() for o, l in zip(so[:2000], sl[:2000])]
+    sa, sof, sle = pack([f.tobytes() for f in frames])
+    want, wext = orc.parse_batch(sa, sof, sle)
+    got, gext = zp.batch.records_to_numpy(r1[idx[:2000]], e1[idx[:2000]])
+    assert_same(got, gext, want, wext)
+    last = offs + lens.to(torch.int64) - 1
+    arena[last] ^= 1
+    r3, _ = zp.batch.parse_batch(arena, offs, lens)
+    torch.cuda.synchronize()
+    assert bool((r3[:, 4] == ERR["IPV4_L4_CHECKSUM"]).all())

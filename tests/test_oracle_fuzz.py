@@ -1,0 +1,55 @@
+"""CPU: mutation fuzz in the style of fuzz/fuzz_targets/fuzz_target_1.rs —
+the C oracle and the independent Python restatement agree on every record
+for mutated golden and generated frames (and neither crashes)."""
+import random
+
+import numpy as np
+
+import oracle as orc
+import pyref
+from test_oracle_golden import ERR
+
+
+def rec_tuple(rec, ext):
+    return (int(rec["err"]), int(rec["flags"]), int(rec["eth_len"]), int(rec["final_nh"]),
+            int(rec["inner_final_nh"]), int(rec["inner_off"]), int(rec["l4_off"]),
+            int(rec["ext_len"]), tuple(int(x) for x in rec["ext_off"]),
+            int(rec["inner_ext_len"]), tuple(int(x) for x in ext["off"]))
+
+
+def mutate(rng, frame):
+    f = bytearray(frame)
+    k = rng.random()
+    if k < 0.5 and f:
+        for _ in range(rng.randint(1, 3)):
+            i = rng.randrange(min(len(f), 160))
+            f[i] = rng.randrange(256)
+    elif k < 0.7 and f:
+        # header-structure bytes: ethertype / version / next-header / lengths
+        i = rng.choice([12, 13, 14, 16, 17, 18, 20, 21, 22, 23]) % len(f)
+        f[i] = rng.choice([0, 4, 6, 17, 41, 43, 44, 51, 58, 59, 60, 0x45, 0x60, 0x81, 0x86, 0xdd,
+                           0x88, 0xa8, 0x08, 0x00, 0xff, 1, 2])
+    elif k < 0.85:
+        f = f[:rng.randrange(len(f) + 1)]
+    else:
+        f += bytes(rng.randrange(256) for _ in range(rng.randint(1, 40)))
+    return bytes(f)
+
+
+def test_fuzz_oracle_vs_pyref(zp, golden):
+    rng = random.Random(1234)
+    seeds = [bytes.fromhex(fx["bytes"]) for fx in golden["fixtures"]]
+    for cfg in ("c3", "c4", "c5"):
+        arena, offs, lens = zp.batch.generate_host(cfg, 40, first=777)
+        seeds += [arena[o:o + l].tobytes() for o, l in zip(offs, lens)]
+    errs = set()
+    for it in range(4000):
+        frame = mutate(rng, rng.choice(seeds))
+        if rng.random() < 0.3:
+            frame = mutate(rng, frame)
+        _, rec, ext = orc.parse_one(frame)
+        got = pyref.to_record_tuple(pyref.parse(frame), ERR)
+        assert rec_tuple(rec, ext) == got, (it, frame.hex())
+        errs.add(int(rec["err"]))
+    # the fuzz reaches a broad set of error paths
+    assert len(errs) >= 18, sorted(errs)

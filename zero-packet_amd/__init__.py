@@ -1,0 +1,22 @@
+"""zero-packet_amd — MI355X-native batched PacketParser::parse.
+
+Import with importlib (the directory name has a hyphen):
+    zp = importlib.import_module("zero-packet_amd")
+
+  zp.batch.parse_batch(arena, offs, lens)   device-resident batch parse (HIP)
+  zp.batch.generate(cfg, n)                  synthetic BASELINE configs on the GPU
+  zp.PacketParser.parse(frame)               one frame through the GPU path
+  zp.PacketParser.from_record(frame, rec)    reference-shaped views over a record
+"""
+from . import _lib, records  # noqa: F401
+from .parser import (ArpReader, AuthenticationHeaderReader, EthernetReader,  # noqa: F401
+                     ExtensionHeaders, FragmentHeaderReader, Icmpv4Reader, Icmpv6Reader,
+                     IpInIp, IPv4Reader, IPv6Reader, OptionsHeaderReader, PacketParser,
+                     RoutingHeaderReader, TcpReader, UdpReader, ZeroPacketError)
+
+try:  # torch-dependent batch API
+    from . import batch  # noqa: F401
+except ImportError:  # pragma: no cover
+    batch = None
+
+__all__ = ["PacketParser", "ZeroPacketError", "batch", "records"]

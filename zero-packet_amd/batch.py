@@ -1,0 +1,94 @@
+"""Device-resident batch API over torch tensors (torch = memory/streams only).
+
+    arena  uint8  [B]       frames packed anywhere in one buffer
+    offs   int64  [n]       frame start offsets (read as uint64)
+    lens   int32  [n]       frame lengths (read as uint32)
+    -> records uint8 [n, 32] (zp_record), optional inner_ext uint8 [n, 12]
+
+parse_batch() enqueues the HIP kernel on torch's current stream of the
+tensors' device (zp_parse_batch_device). No CPU fallback: non-CUDA tensors or
+a missing libzp_hip.so raise.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from .records import EXT_DTYPE, RECORD_DTYPE
+
+CONFIGS = {"c1": 1, "c2": 2, "c3": 3, "c4": 4, "c5": 5}
+SEED = 0x5EED2025
+
+
+def _stream_ptr(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _need_cuda(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("zero-packet_amd batch API needs device tensors (no CPU fallback)")
+
+
+def parse_batch(arena, offs, lens, records=None, inner_ext=None, stream=None):
+    """Parses every frame; returns (records, inner_ext) as uint8 device tensors."""
+    _need_cuda(arena, offs, lens)
+    n = offs.numel()
+    assert lens.numel() == n and offs.dtype == torch.int64 and lens.dtype == torch.int32
+    assert arena.dtype == torch.uint8 and arena.is_contiguous()
+    dev = arena.device
+    if records is None:
+        records = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+    if inner_ext is None:
+        inner_ext = torch.zeros((n, 12), dtype=torch.uint8, device=dev)
+    s = ctypes.c_void_p(stream) if stream is not None else _stream_ptr(dev)
+    rc = _lib.hip().zp_parse_batch_device(arena.data_ptr(), offs.data_ptr(), lens.data_ptr(), n,
+                                          records.data_ptr(), inner_ext.data_ptr(), s)
+    _lib.check(rc, "zp_parse_batch_device")
+    return records, inner_ext
+
+
+def generate(config, n, seed=SEED, first=0, device="cuda", pad=64):
+    """Synthetic batch of BASELINE config `config` on the GPU: packets
+    first..first+n-1, packed back to back. Returns (arena, offs, lens)."""
+    cfg = CONFIGS.get(config, config)
+    dev = torch.device(device)
+    lens = torch.empty(n, dtype=torch.int32, device=dev)
+    s = _stream_ptr(dev)
+    _lib.check(_lib.hip().zp_gen_lengths_device(cfg, seed, first, n, lens.data_ptr(), s),
+               "zp_gen_lengths_device")
+    offs = torch.zeros(n, dtype=torch.int64, device=dev)
+    if n > 1:
+        torch.cumsum(lens[:-1].to(torch.int64), 0, out=offs[1:])
+    total = int(offs[-1].item() + lens[-1].item()) if n else 0
+    arena = torch.zeros(total + pad, dtype=torch.uint8, device=dev)
+    _lib.check(_lib.hip().zp_gen_frames_device(cfg, seed, first, n, arena.data_ptr(),
+                                               offs.data_ptr(), lens.data_ptr(), s),
+               "zp_gen_frames_device")
+    return arena, offs, lens
+
+
+def generate_host(config, n, seed=SEED, first=0, nthreads=0, pad=64):
+    """CPU build of the same generator (libzp_host.so): numpy arrays."""
+    cfg = CONFIGS.get(config, config)
+    lens = np.empty(n, dtype=np.uint32)
+    _lib.host().zp_host_gen_lengths(cfg, seed, first, n, lens.ctypes.data)
+    offs = np.zeros(n, dtype=np.uint64)
+    if n > 1:
+        offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    total = int(offs[-1] + lens[-1]) if n else 0
+    arena = np.zeros(total + pad, dtype=np.uint8)
+    _lib.host().zp_host_gen_frames(cfg, seed, first, n, arena.ctypes.data, offs.ctypes.data,
+                                   nthreads)
+    return arena, offs, lens
+
+
+def records_to_numpy(records, inner_ext=None):
+    """uint8 [n,32] (device or host) -> structured numpy (RECORD_DTYPE)."""
+    r = records.cpu().numpy() if isinstance(records, torch.Tensor) else records
+    rec = np.ascontiguousarray(r).view(RECORD_DTYPE).reshape(-1)
+    if inner_ext is None:
+        return rec
+    e = inner_ext.cpu().numpy() if isinstance(inner_ext, torch.Tensor) else inner_ext
+    return rec, np.ascontiguousarray(e).view(EXT_DTYPE).reshape(-1)

@@ -1,0 +1,222 @@
+// zp_ctx.hip — host-memory entry points of the C ABI (zero_packet.h):
+// zp_ctx_create / zp_ctx_destroy / zp_parse_batch_host / zp_parse_one.
+//
+// Frames arrive in host memory (a NIC ring / raw socket buffer,
+// README.md:85-115 of the reference). The batch is cut into chunks whose byte
+// span fits the device staging buffer; two slots on two streams overlap
+// chunk k's H2D copy and parse with chunk k-1's D2H copy. Pinned user
+// buffers are DMA'd directly; pageable ones are staged through pinned
+// memory. The parse itself is the device kernel (zp_parse.hip); there is no
+// host-side parse.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../include/zero_packet.h"
+
+// Thread-local error text shared with zp_parse.hip (read via zp_last_error()).
+extern "C" char* zp__errbuf(void);
+#define g_ctx_error (zp__errbuf())
+#define ERRBUF_LEN 256
+
+#define SLOTS 2
+
+struct zp_ctx {
+    int device;
+    uint64_t chunk_bytes, chunk_pkts;
+    hipStream_t s[SLOTS];
+    hipEvent_t ev[SLOTS];
+    uint8_t* d_arena[SLOTS];
+    uint64_t* d_offs[SLOTS];
+    uint32_t* d_lens[SLOTS];
+    zp_record* d_rec[SLOTS];
+    zp_ext_offsets* d_ext[SLOTS];
+    uint8_t* h_arena[SLOTS];      // pinned staging
+    uint64_t* h_offs[SLOTS];
+    uint32_t* h_lens[SLOTS];
+    zp_record* h_rec[SLOTS];
+    zp_ext_offsets* h_ext[SLOTS];
+};
+
+#define TRY(x)                                                                     \
+    do {                                                                           \
+        hipError_t e_ = (x);                                                       \
+        if (e_ != hipSuccess) {                                                    \
+            snprintf(g_ctx_error, ERRBUF_LEN, "%s: %s", #x,                \
+                     hipGetErrorString(e_));                                       \
+            fprintf(stderr, "zero-packet: %s\n", g_ctx_error);                     \
+            goto fail;                                                             \
+        }                                                                          \
+    } while (0)
+
+extern "C" void zp_ctx_destroy(zp_ctx* c) {
+    if (!c) return;
+    int prev = 0;
+    hipGetDevice(&prev);
+    hipSetDevice(c->device);
+    for (int k = 0; k < SLOTS; ++k) {
+        if (c->s[k]) hipStreamSynchronize(c->s[k]);
+        hipFree(c->d_arena[k]); hipFree(c->d_offs[k]); hipFree(c->d_lens[k]);
+        hipFree(c->d_rec[k]); hipFree(c->d_ext[k]);
+        hipHostFree(c->h_arena[k]); hipHostFree(c->h_offs[k]); hipHostFree(c->h_lens[k]);
+        hipHostFree(c->h_rec[k]); hipHostFree(c->h_ext[k]);
+        if (c->ev[k]) hipEventDestroy(c->ev[k]);
+        if (c->s[k]) hipStreamDestroy(c->s[k]);
+    }
+    hipSetDevice(prev);
+    free(c);
+}
+
+extern "C" zp_ctx* zp_ctx_create(int device, uint64_t chunk_bytes) {
+    zp_ctx* c = (zp_ctx*)calloc(1, sizeof(zp_ctx));
+    int prev = 0;
+    if (!c) return NULL;
+    if (chunk_bytes == 0) chunk_bytes = 256ull << 20;
+    if (chunk_bytes < 65536) chunk_bytes = 65536;
+    c->device = device;
+    c->chunk_bytes = chunk_bytes;
+    c->chunk_pkts = chunk_bytes / 64 + 1;
+    hipGetDevice(&prev);
+    TRY(hipSetDevice(device));
+    for (int k = 0; k < SLOTS; ++k) {
+        TRY(hipStreamCreateWithFlags(&c->s[k], hipStreamNonBlocking));
+        TRY(hipEventCreateWithFlags(&c->ev[k], hipEventDisableTiming));
+        TRY(hipMalloc(&c->d_arena[k], chunk_bytes + 64));
+        TRY(hipMalloc(&c->d_offs[k], c->chunk_pkts * sizeof(uint64_t)));
+        TRY(hipMalloc(&c->d_lens[k], c->chunk_pkts * sizeof(uint32_t)));
+        TRY(hipMalloc(&c->d_rec[k], c->chunk_pkts * sizeof(zp_record)));
+        TRY(hipMalloc(&c->d_ext[k], c->chunk_pkts * sizeof(zp_ext_offsets)));
+        TRY(hipHostMalloc(&c->h_arena[k], chunk_bytes + 64, hipHostMallocDefault));
+        TRY(hipHostMalloc(&c->h_offs[k], c->chunk_pkts * sizeof(uint64_t), hipHostMallocDefault));
+        TRY(hipHostMalloc(&c->h_lens[k], c->chunk_pkts * sizeof(uint32_t), hipHostMallocDefault));
+        TRY(hipHostMalloc(&c->h_rec[k], c->chunk_pkts * sizeof(zp_record), hipHostMallocDefault));
+        TRY(hipHostMalloc(&c->h_ext[k], c->chunk_pkts * sizeof(zp_ext_offsets), hipHostMallocDefault));
+    }
+    hipSetDevice(prev);
+    return c;
+fail:
+    hipSetDevice(prev);
+    zp_ctx_destroy(c);
+    return NULL;
+}
+
+static bool is_pinned(const void* p) {
+    hipPointerAttribute_t a;
+    hipError_t e = hipPointerGetAttributes(&a, p);
+    if (e != hipSuccess) { (void)hipGetLastError(); return false; }
+    return a.type == hipMemoryTypeHost;
+}
+
+struct Pending { uint64_t i, j; bool live; };
+
+// Copies a finished slot's results to the user arrays.
+static int drain(zp_ctx* c, int k, Pending& pd, zp_record* recs, zp_ext_offsets* ext,
+                 bool rec_direct) {
+    if (!pd.live) return 0;
+    hipError_t e = hipEventSynchronize(c->ev[k]);
+    if (e != hipSuccess) {
+        snprintf(g_ctx_error, ERRBUF_LEN, "hipEventSynchronize: %s", hipGetErrorString(e));
+        return -2;
+    }
+    uint64_t m = pd.j - pd.i;
+    if (!rec_direct) memcpy(recs + pd.i, c->h_rec[k], m * sizeof(zp_record));
+    if (ext) {
+        for (uint64_t q = 0; q < m; ++q)
+            if (recs[pd.i + q].flags & ZP_F_INNER_EXT) ext[pd.i + q] = c->h_ext[k][q];
+    }
+    pd.live = false;
+    return 0;
+}
+
+extern "C" int zp_parse_batch_device(const uint8_t*, const uint64_t*, const uint32_t*, uint64_t,
+                                     zp_record*, zp_ext_offsets*, void*);
+
+extern "C" int zp_parse_batch_host(zp_ctx* c, const uint8_t* arena, uint64_t arena_bytes,
+                                   const uint64_t* offs, const uint32_t* lens, uint64_t n,
+                                   zp_record* recs, zp_ext_offsets* ext) {
+    if (!c || (n && (!arena || !offs || !lens || !recs))) return -1;
+    if (n == 0) return 0;
+    int prev = 0;
+    int rc = 0;
+    hipGetDevice(&prev);
+    if (hipSetDevice(c->device) != hipSuccess) return -2;
+    const bool arena_direct = is_pinned(arena);
+    const bool rec_direct = is_pinned(recs);
+    Pending pd[SLOTS] = {{0, 0, false}, {0, 0, false}};
+    uint64_t i = 0;
+    int k = 0;
+    while (i < n) {
+        // Chunk [i, j) with byte span [lo, hi) <= chunk_bytes.
+        uint64_t lo = offs[i], hi = offs[i] + lens[i];
+        if (hi - lo > c->chunk_bytes) {
+            snprintf(g_ctx_error, ERRBUF_LEN,
+                     "frame %llu (%u B) exceeds the context chunk size",
+                     (unsigned long long)i, lens[i]);
+            rc = -3;
+            break;
+        }
+        if (arena_bytes && hi > arena_bytes) {
+            snprintf(g_ctx_error, ERRBUF_LEN, "frame %llu lies outside the arena",
+                     (unsigned long long)i);
+            rc = -1;
+            break;
+        }
+        uint64_t j = i + 1;
+        while (j < n && j - i < c->chunk_pkts) {
+            uint64_t l2 = offs[j] < lo ? offs[j] : lo;
+            uint64_t h2 = offs[j] + lens[j] > hi ? offs[j] + lens[j] : hi;
+            if (h2 - l2 > c->chunk_bytes || (arena_bytes && h2 > arena_bytes)) break;
+            lo = l2; hi = h2; ++j;
+        }
+        if ((rc = drain(c, k, pd[k], recs, ext, rec_direct)) != 0) break;
+        uint64_t m = j - i;
+        for (uint64_t q = 0; q < m; ++q) {
+            c->h_offs[k][q] = offs[i + q] - lo;
+            c->h_lens[k][q] = lens[i + q];
+        }
+        const uint8_t* src = arena + lo;
+        if (!arena_direct) { memcpy(c->h_arena[k], src, hi - lo); src = c->h_arena[k]; }
+        hipStream_t s = c->s[k];
+        hipMemcpyAsync(c->d_arena[k], src, hi - lo, hipMemcpyHostToDevice, s);
+        hipMemcpyAsync(c->d_offs[k], c->h_offs[k], m * 8, hipMemcpyHostToDevice, s);
+        hipMemcpyAsync(c->d_lens[k], c->h_lens[k], m * 4, hipMemcpyHostToDevice, s);
+        rc = zp_parse_batch_device(c->d_arena[k], c->d_offs[k], c->d_lens[k], m, c->d_rec[k],
+                                   ext ? c->d_ext[k] : NULL, s);
+        if (rc) break;
+        hipMemcpyAsync(rec_direct ? (void*)(recs + i) : (void*)c->h_rec[k], c->d_rec[k],
+                       m * sizeof(zp_record), hipMemcpyDeviceToHost, s);
+        if (ext)
+            hipMemcpyAsync(c->h_ext[k], c->d_ext[k], m * sizeof(zp_ext_offsets),
+                           hipMemcpyDeviceToHost, s);
+        hipError_t e = hipEventRecord(c->ev[k], s);
+        if (e != hipSuccess) {
+            snprintf(g_ctx_error, ERRBUF_LEN, "hipEventRecord: %s", hipGetErrorString(e));
+            rc = -2;
+            break;
+        }
+        pd[k] = Pending{i, j, true};
+        i = j;
+        k = (k + 1) % SLOTS;
+    }
+    for (int q = 0; q < SLOTS; ++q) {
+        int r2 = drain(c, (k + q) % SLOTS, pd[(k + q) % SLOTS], recs, ext, rec_direct);
+        if (!rc) rc = r2;
+    }
+    hipSetDevice(prev);
+    return rc;
+}
+
+extern "C" int zp_parse_one(zp_ctx* c, const uint8_t* frame, uint64_t len,
+                            zp_record* record, zp_ext_offsets* inner_ext) {
+    uint64_t off = 0;
+    uint32_t l = (uint32_t)len;
+    if (len > 0xFFFFFFFFull) return -1;
+    static const uint8_t empty[16] = {0};
+    if (!frame) frame = empty;
+    int rc = zp_parse_batch_host(c, frame, len, &off, &l, 1, record, inner_ext);
+    if (rc) return rc;
+    return record->err;
+}

@@ -1,0 +1,469 @@
+"""PacketParser / *Reader facade over zp_record (the reference's public API).
+
+Mirrors src/packet/parser.rs:22-69 and the reader views of src/datalink,
+src/network and src/transport: field names, getters and `Result` errors
+(raised as ZeroPacketError carrying the exact reference string). Every
+reader is a view `frame[start:]` that runs to the end of the frame, exactly
+like the reference's `&'a [u8]` sub-slices, so a PacketParser is rebuilt from
+a record without re-parsing (PacketParser.from_record).
+
+PacketParser.parse(frame) parses through the GPU (zp_parse_one); batches go
+through zero-packet_amd.batch. There is no CPU parse path in this package.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from .records import (EXT_DTYPE, EXT_SLOTS, F_ARP, F_ETHERNET, F_EXT, F_EXT_SLOT, F_ICMPV4,
+                      F_ICMPV6, F_INNER_EXT, F_INNER_EXT_SLOT, F_IP_IN_IP, F_IP_IN_IP_V6,
+                      F_IPV4, F_IPV6, F_TCP, F_UDP, RECORD_DTYPE)
+
+
+class ZeroPacketError(Exception):
+    """Err(&'static str) of the reference; .code is the zp_err value."""
+
+    def __init__(self, message, code=None):
+        super().__init__(message)
+        self.code = code
+
+
+def _be16(b, i):
+    return (b[i] << 8) | b[i + 1]
+
+
+def _be32(b, i):
+    return (b[i] << 24) | (b[i + 1] << 16) | (b[i + 2] << 8) | b[i + 3]
+
+
+def _internet_checksum(data, acc=0):
+    s = acc & 0xFFFFFFFF
+    n = len(data) & ~1
+    for i in range(0, n, 2):
+        s = (s + ((data[i] << 8) | data[i + 1])) & 0xFFFFFFFF
+    if len(data) & 1:
+        s = (s + (data[-1] << 8)) & 0xFFFFFFFF
+    while s >> 16:
+        s = (s & 0xFFFF) + (s >> 16)
+    return (~s) & 0xFFFF
+
+
+class _Reader:
+    def __init__(self, data):
+        self.bytes = bytes(data)
+
+    def __eq__(self, other):
+        return type(self) is type(other) and self.bytes == other.bytes
+
+
+class EthernetReader(_Reader):
+    """ethernet.rs:131-263."""
+
+    def __init__(self, data, header_len=None):
+        super().__init__(data)
+        if len(self.bytes) < 14:
+            raise ZeroPacketError("Slice is too short to contain an Ethernet frame.", 2)
+        self._hl = header_len if header_len is not None else self.calculate_header_len(self.bytes)
+
+    @staticmethod
+    def calculate_header_len(b):
+        t = _be16(b, 12)
+        if t == 0x8100:
+            if len(b) < 18:
+                raise ZeroPacketError("Slice is too short to contain VLAN tagging.", 3)
+            return 18
+        if t == 0x88A8:
+            if len(b) < 22:
+                raise ZeroPacketError("Slice is too short to contain double VLAN tagging.", 4)
+            if _be16(b, 16) != 0x8100:
+                raise ZeroPacketError("Invalid double VLAN tag.", 5)
+            return 22
+        return 14
+
+    @staticmethod
+    def is_vlan_tagged(b):
+        return _be16(b, 12) == 0x8100
+
+    @staticmethod
+    def is_vlan_double_tagged(b):
+        return _be16(b, 12) == 0x88A8
+
+    def dest_mac(self):
+        return self.bytes[0:6]
+
+    def src_mac(self):
+        return self.bytes[6:12]
+
+    def ethertype(self):
+        return _be16(self.bytes, self._hl - 2)
+
+    def vlan_tag(self):
+        if not self.is_vlan_tagged(self.bytes):
+            return None
+        return (_be16(self.bytes, 12), _be16(self.bytes, 14))
+
+    def double_vlan_tag(self):
+        if not self.is_vlan_double_tagged(self.bytes):
+            return None
+        b = self.bytes
+        return ((_be16(b, 12), _be16(b, 14)), (_be16(b, 16), _be16(b, 18)))
+
+    def header_len(self):
+        return self._hl
+
+    def header(self):
+        return self.bytes[:self._hl]
+
+    def payload(self):
+        return self.bytes[self._hl:]
+
+
+class ArpReader(_Reader):
+    """arp.rs:121-227."""
+
+    def htype(self): return _be16(self.bytes, 0)
+    def ptype(self): return _be16(self.bytes, 2)
+    def hlen(self): return self.bytes[4]
+    def plen(self): return self.bytes[5]
+    def oper(self): return _be16(self.bytes, 6)
+    def sha(self): return self.bytes[8:14]
+    def spa(self): return self.bytes[14:18]
+    def tha(self): return self.bytes[18:24]
+    def tpa(self): return self.bytes[24:28]
+    def header_len(self): return 28
+    def header(self): return self.bytes[:28]
+    def payload(self): return self.bytes[28:]
+
+
+class IPv4Reader(_Reader):
+    """ipv4.rs:129-265."""
+
+    def version(self): return self.bytes[0] >> 4
+    def ihl(self): return self.bytes[0] & 0x0F
+    def dscp(self): return self.bytes[1] >> 2
+    def ecn(self): return self.bytes[1] & 0x03
+    def total_length(self): return _be16(self.bytes, 2)
+    def id(self): return _be16(self.bytes, 4)
+    def flags(self): return self.bytes[6] >> 5
+    def fragment_offset(self): return ((self.bytes[6] & 0x1F) << 8) | self.bytes[7]
+    def ttl(self): return self.bytes[8]
+    def protocol(self): return self.bytes[9]
+    def src_ip(self): return self.bytes[12:16]
+    def dest_ip(self): return self.bytes[16:20]
+    def checksum(self): return _be16(self.bytes, 10)
+    def header_len(self): return self.ihl() * 4
+
+    def header(self):
+        if self.header_len() > len(self.bytes):
+            raise ZeroPacketError("Indicated IPv4 header length exceeds the allocated buffer.", 14)
+        return self.bytes[:self.header_len()]
+
+    def payload(self):
+        if self.header_len() > len(self.bytes):
+            raise ZeroPacketError("Indicated IPv4 header length exceeds the allocated buffer.", 14)
+        return self.bytes[self.header_len():]
+
+    def valid_checksum(self):
+        return _internet_checksum(self.header(), 0) == 0
+
+
+class OptionsHeaderReader(_Reader):
+    """extensions/options.rs:76-154 (Hop-by-Hop / Destination Options)."""
+
+    def next_header(self): return self.bytes[0]
+    def header_ext_len(self): return self.bytes[1]
+    def header_len(self): return (self.bytes[1] + 1) * 8
+
+    def options(self):
+        if len(self.bytes) < self.header_len():
+            raise ZeroPacketError("Indicated header length exceeds the allocated buffer.")
+        return self.bytes[2:self.header_len()]
+
+    def header(self):
+        if self.header_len() > len(self.bytes):
+            raise ZeroPacketError(
+                "Indicated IPv6 options header length exceeds the allocated buffer.", 19)
+        return self.bytes[:self.header_len()]
+
+    def payload(self):
+        if self.header_len() > len(self.bytes):
+            raise ZeroPacketError(
+                "Indicated IPv6 options header length exceeds the allocated buffer.", 19)
+        return self.bytes[self.header_len():]
+
+
+class RoutingHeaderReader(_Reader):
+    """extensions/routing.rs:99-195."""
+
+    def next_header(self): return self.bytes[0]
+    def header_ext_len(self): return self.bytes[1]
+    def routing_type(self): return self.bytes[2]
+    def segments_left(self): return self.bytes[3]
+    def data(self): return self.bytes[4:self.header_len()]
+    def header_len(self): return (self.bytes[1] + 1) * 8
+
+    def header(self):
+        if self.header_len() > len(self.bytes):
+            raise ZeroPacketError(
+                "Indicated IPv6 routing header length exceeds the allocated buffer.", 21)
+        return self.bytes[:self.header_len()]
+
+    def payload(self):
+        if self.header_len() > len(self.bytes):
+            raise ZeroPacketError(
+                "Indicated IPv6 routing header length exceeds the allocated buffer.", 21)
+        return self.bytes[self.header_len():]
+
+
+class FragmentHeaderReader(_Reader):
+    """extensions/fragment.rs:90-173."""
+
+    def next_header(self): return self.bytes[0]
+    def reserved(self): return self.bytes[1]
+    def fragment_offset(self): return (self.bytes[2] << 5) | (self.bytes[3] & 0x1F)
+    def res(self): return (self.bytes[3] >> 5) & 0b11
+    def m_flag(self): return (self.bytes[3] & 0x80) != 0
+    def identification(self): return _be32(self.bytes, 4)
+    def header_len(self): return 8
+    def header(self): return self.bytes[:8]
+    def payload(self): return self.bytes[8:]
+
+
+class AuthenticationHeaderReader(_Reader):
+    """extensions/authentication.rs:97-200."""
+
+    def next_header(self): return self.bytes[0]
+    def payload_len(self): return self.bytes[1]
+    def reserved(self): return _be16(self.bytes, 2)
+    def spi(self): return _be32(self.bytes, 4)
+    def sequence_number(self): return _be32(self.bytes, 8)
+    def header_len(self): return (self.bytes[1] + 2) * 4
+
+    def authentication_data(self):
+        if len(self.bytes) < self.header_len():
+            raise ZeroPacketError(
+                "Indicated Authentication header length exceeds the allocated buffer.", 24)
+        return self.bytes[12:self.header_len()]
+
+    def header(self):
+        if self.header_len() > len(self.bytes):
+            raise ZeroPacketError(
+                "Indicated Authentication header length exceeds the allocated buffer.", 24)
+        return self.bytes[:self.header_len()]
+
+    def payload(self):
+        if self.header_len() > len(self.bytes):
+            raise ZeroPacketError(
+                "Indicated Authentication header length exceeds the allocated buffer.", 24)
+        return self.bytes[self.header_len():]
+
+
+_EXT_CLS = [OptionsHeaderReader, RoutingHeaderReader, FragmentHeaderReader,
+            AuthenticationHeaderReader, OptionsHeaderReader, OptionsHeaderReader]
+
+
+class ExtensionHeaders:
+    """extensions/headers.rs:19-28."""
+
+    def __init__(self):
+        self.hop_by_hop = self.routing = self.fragment = None
+        self.auth_header = self.destination_1st = self.destination_2nd = None
+        self.total_headers_len = 0
+        self.final_next_header = 0
+
+
+class IPv6Reader(_Reader):
+    """ipv6.rs:135-286. Built from a record: extension headers come from the
+    record's offsets instead of a re-walk."""
+
+    def __init__(self, data, extension_headers=None, extension_headers_len=0):
+        super().__init__(data)
+        self.extension_headers = extension_headers
+        self.extension_headers_len = extension_headers_len
+
+    def version(self): return self.bytes[0] >> 4
+    def traffic_class(self): return ((self.bytes[0] & 0x0F) << 4) | (self.bytes[1] >> 4)
+
+    def flow_label(self):
+        return ((self.bytes[1] & 0x0F) << 16) | (self.bytes[2] << 8) | self.bytes[3]
+
+    def payload_length(self): return _be16(self.bytes, 4)
+    def next_header(self): return self.bytes[6]
+
+    def final_next_header(self):
+        if self.extension_headers is not None:
+            return self.extension_headers.final_next_header
+        return self.next_header()
+
+    def hop_limit(self): return self.bytes[7]
+    def src_addr(self): return self.bytes[8:24]
+    def dest_addr(self): return self.bytes[24:40]
+    def header_len(self): return 40
+    def header(self): return self.bytes[:40]
+    def payload(self): return self.bytes[40:]
+    def upper_layer_payload(self): return self.bytes[40 + self.extension_headers_len:]
+
+
+class TcpReader(_Reader):
+    """tcp.rs:132-244."""
+
+    def src_port(self): return _be16(self.bytes, 0)
+    def dest_port(self): return _be16(self.bytes, 2)
+    def sequence_number(self): return _be32(self.bytes, 4)
+    def ack_number(self): return _be32(self.bytes, 8)
+    def data_offset(self): return self.bytes[12] >> 4
+    def reserved(self): return self.bytes[12] & 0x0F
+    def flags(self): return self.bytes[13]
+    def window_size(self): return _be16(self.bytes, 14)
+    def checksum(self): return _be16(self.bytes, 16)
+    def urgent_pointer(self): return _be16(self.bytes, 18)
+    def header_len(self): return self.data_offset() * 4
+
+    def header(self):
+        if self.header_len() > len(self.bytes):
+            raise ZeroPacketError("Indicated TCP header length exceeds the allocated buffer.")
+        return self.bytes[:self.header_len()]
+
+    def payload(self):
+        if self.header_len() > len(self.bytes):
+            raise ZeroPacketError("Indicated TCP header length exceeds the allocated buffer.")
+        return self.bytes[self.header_len():]
+
+
+class UdpReader(_Reader):
+    """udp.rs:94-154."""
+
+    def src_port(self): return _be16(self.bytes, 0)
+    def dest_port(self): return _be16(self.bytes, 2)
+    def checksum(self): return _be16(self.bytes, 6)
+    def length(self): return _be16(self.bytes, 4)
+    def header_len(self): return 8
+    def header(self): return self.bytes[:8]
+    def payload(self): return self.bytes[8:]
+
+
+class _IcmpReader(_Reader):
+    def icmp_type(self): return self.bytes[0]
+    def icmp_code(self): return self.bytes[1]
+    def checksum(self): return _be16(self.bytes, 2)
+    def header_len(self): return 8
+    def header(self): return self.bytes[:8]
+    def payload(self): return self.bytes[8:]
+
+
+class Icmpv4Reader(_IcmpReader):
+    """icmpv4.rs:83-135."""
+
+
+class Icmpv6Reader(_IcmpReader):
+    """icmpv6.rs:80-132."""
+
+
+class IpInIp:
+    """misc.rs:6-9: IpInIp::Ipv4(IPv4Reader) | IpInIp::Ipv6(IPv6Reader)."""
+
+    def __init__(self, kind, reader):
+        self.kind = kind          # "ipv4" or "ipv6"
+        self.reader = reader
+
+    def __repr__(self):
+        return f"IpInIp::{'Ipv4' if self.kind == 'ipv4' else 'Ipv6'}"
+
+
+def _ext_from(frame, payload_off, flags, shift, offs, total, final_nh):
+    eh = ExtensionHeaders()
+    for k, name in enumerate(EXT_SLOTS):
+        if flags & (1 << (shift + k)):
+            setattr(eh, name, _EXT_CLS[k](frame[payload_off + int(offs[k]):]))
+    eh.total_headers_len = int(total)
+    eh.final_next_header = int(final_nh)
+    return eh
+
+
+class PacketParser:
+    """parser.rs:22-32. Fields are None or reader views."""
+
+    FIELDS = ("ethernet", "arp", "ipv4", "ipv6", "ip_in_ip", "tcp", "udp", "icmpv4", "icmpv6")
+
+    def __init__(self):
+        for f in self.FIELDS:
+            setattr(self, f, None)
+
+    @classmethod
+    def from_record(cls, frame, rec, inner_ext=None):
+        """Rebuilds the parser of `frame` from its zp_record (no re-parse).
+        Raises ZeroPacketError when the record holds an error."""
+        frame = bytes(frame)
+        err = int(rec["err"])
+        if err:
+            raise ZeroPacketError(_lib.hip().zp_err_str(err).decode() if _lib_available()
+                                  else f"zp_err {err}", err)
+        flags = int(rec["flags"])
+        p = cls()
+        hl = int(rec["eth_len"])
+        if flags & F_ETHERNET:
+            p.ethernet = EthernetReader(frame, hl)
+        if flags & F_ARP:
+            p.arp = ArpReader(frame[hl:])
+        if flags & F_IPV4:
+            p.ipv4 = IPv4Reader(frame[hl:])
+        if flags & F_IPV6:
+            eh = None
+            if flags & F_EXT:
+                eh = _ext_from(frame, hl + 40, flags, 12, rec["ext_off"], rec["ext_len"],
+                               rec["final_nh"])
+            p.ipv6 = IPv6Reader(frame[hl:], eh, int(rec["ext_len"]) if eh else 0)
+        if flags & F_IP_IN_IP:
+            io = int(rec["inner_off"])
+            if flags & F_IP_IN_IP_V6:
+                eh = None
+                if flags & F_INNER_EXT:
+                    offs = inner_ext["off"] if inner_ext is not None else [0] * 6
+                    eh = _ext_from(frame, io + 40, flags, 18, offs, rec["inner_ext_len"],
+                                   rec["inner_final_nh"])
+                p.ip_in_ip = IpInIp("ipv6", IPv6Reader(frame[io:], eh,
+                                                       int(rec["inner_ext_len"]) if eh else 0))
+            else:
+                p.ip_in_ip = IpInIp("ipv4", IPv4Reader(frame[io:]))
+        l4 = int(rec["l4_off"])
+        if flags & F_TCP:
+            p.tcp = TcpReader(frame[l4:])
+        if flags & F_UDP:
+            p.udp = UdpReader(frame[l4:])
+        if flags & F_ICMPV4:
+            p.icmpv4 = Icmpv4Reader(frame[l4:])
+        if flags & F_ICMPV6:
+            p.icmpv6 = Icmpv6Reader(frame[l4:])
+        return p
+
+    @classmethod
+    def parse(cls, frame):
+        """PacketParser::parse (parser.rs:53) through the GPU path."""
+        frame = bytes(frame)
+        rec = np.zeros(1, RECORD_DTYPE)
+        ext = np.zeros(1, EXT_DTYPE)
+        buf = ctypes.create_string_buffer(frame, len(frame) or 1)
+        rc = _lib.hip().zp_parse_one(_default_ctx(), ctypes.addressof(buf), len(frame),
+                                     rec.ctypes.data, ext.ctypes.data)
+        _lib.check(rc, "zp_parse_one")
+        return cls.from_record(frame, rec[0], ext[0])
+
+
+def _lib_available():
+    try:
+        _lib.hip()
+        return True
+    except Exception:
+        return False
+
+
+_CTX = None
+
+
+def _default_ctx():
+    global _CTX
+    if _CTX is None:
+        _CTX = _lib.hip().zp_ctx_create(0, 0)
+        if not _CTX:
+            raise RuntimeError("zp_ctx_create failed: " + _lib.hip().zp_last_error().decode())
+    return _CTX

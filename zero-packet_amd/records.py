@@ -1,0 +1,42 @@
+"""zp_record layout (include/zero_packet.h) as a numpy structured dtype."""
+import numpy as np
+
+RECORD_DTYPE = np.dtype([
+    ("flags", "<u4"), ("err", "u1"), ("eth_len", "u1"), ("final_nh", "u1"),
+    ("inner_final_nh", "u1"), ("inner_off", "<u4"), ("l4_off", "<u4"),
+    ("ext_len", "<u2"), ("ext_off", "<u2", (6,)), ("inner_ext_len", "<u2"),
+])
+assert RECORD_DTYPE.itemsize == 32
+EXT_DTYPE = np.dtype([("off", "<u2", (6,))])
+assert EXT_DTYPE.itemsize == 12
+
+# Presence bits (zero_packet.h ZP_F_*).
+F_ETHERNET, F_ARP, F_IPV4, F_IPV6 = 1 << 0, 1 << 1, 1 << 2, 1 << 3
+F_IP_IN_IP, F_IP_IN_IP_V6 = 1 << 4, 1 << 5
+F_TCP, F_UDP, F_ICMPV4, F_ICMPV6 = 1 << 6, 1 << 7, 1 << 8, 1 << 9
+F_EXT, F_INNER_EXT = 1 << 10, 1 << 11
+EXT_SLOTS = ["hop_by_hop", "routing", "fragment", "auth_header",
+             "destination_1st", "destination_2nd"]
+
+
+def F_EXT_SLOT(k):
+    return 1 << (12 + k)
+
+
+def F_INNER_EXT_SLOT(k):
+    return 1 << (18 + k)
+
+
+# zp_err codes, in enum order (zero_packet.h).
+ERR_NAMES = [
+    "OK", "ETH_FRAME_TOO_SHORT", "ETH_SLICE_TOO_SHORT", "ETH_VLAN_TOO_SHORT",
+    "ETH_QINQ_TOO_SHORT", "ETH_INVALID_QINQ", "ARP_TOO_SHORT", "ARP_INVALID_OPER",
+    "IPV4_TOO_SHORT", "IPV4_VERSION", "IPV4_IHL_TOO_SHORT", "IPV4_HDR_TOO_LONG",
+    "IPV4_TOTAL_LENGTH", "IPV4_CHECKSUM", "IPV4_HDR_EXCEEDS", "IPV6_TOO_SHORT",
+    "IPV6_VERSION", "EXT_HBH_NOT_FIRST", "EXT_OPTIONS_TOO_SHORT", "EXT_OPTIONS_EXCEEDS",
+    "EXT_ROUTING_TOO_SHORT", "EXT_ROUTING_EXCEEDS", "EXT_FRAGMENT_TOO_SHORT",
+    "EXT_AUTH_TOO_SHORT", "EXT_AUTH_EXCEEDS", "TCP_TOO_SHORT", "TCP_DATA_OFFSET",
+    "TCP_FLAGS", "UDP_TOO_SHORT", "UDP_LENGTH", "ICMP_TOO_SHORT", "ICMPV4_TYPE",
+    "ICMPV4_CODE", "ICMPV6_TYPE", "IPV4_L4_CHECKSUM", "IPV6_L4_CHECKSUM",
+]
+ERR = {name: i for i, name in enumerate(ERR_NAMES)}
