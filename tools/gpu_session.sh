@@ -16,13 +16,15 @@ step() {  # step <name> <timeout> <cmd...>
   if [ $rc -ge 124 ]; then echo "fatal rc=$rc in $name, stopping" | tee -a $OUT/session.log; exit $rc; fi
   return 0
 }
+i=0
 for s in "$@"; do
+  i=$((i+1))
   case $s in
     build)  step build 600 python __graft_entry__.py ;;
     tests)  step gpu_tests 1200 python -m pytest tests -m gpu -q -p no:cacheprovider --timeout 600 ;;
     smoke)  step smoke 300 python __graft_entry__.py smoke ;;
     bench)  step bench 900 python bench.py ;;
     prof)   step prof 900 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --steps 10 --no-cpu --no-pcie ;;
-    *) step custom 900 bash -c "$s" ;;
+    *) step "step$i" 900 bash -c "$s" ;;
   esac
 done

@@ -1,0 +1,96 @@
+"""Kernel A/B harness (one process, interleaved rounds; guide §5.4 rule 24).
+
+    python tools/kbench.py [--configs c3,c2,c4,c5] [--variants base,...] [--membw]
+
+Variants are extra builds of zp_parse.hip (tools/build_variants.sh) exposing
+the same C ABI; each is timed with HIP events on the same resident batch.
+"""
+import argparse
+import ctypes
+import glob
+import importlib
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def time_launches(fn, reps):
+    s = torch.cuda.current_stream()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(reps)]
+    for a, b in ev:
+        a.record(s)
+        fn()
+        b.record(s)
+    torch.cuda.synchronize()
+    return [a.elapsed_time(b) for a, b in ev]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="c3,c2,c4,c5")
+    ap.add_argument("--variants", default="")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--membw", action="store_true")
+    args = ap.parse_args()
+    zp = importlib.import_module("zero-packet_amd")
+    dev = torch.device("cuda:0")
+    libs = {"base": zp._lib.hip()}
+    for v in [x for x in args.variants.split(",") if x]:
+        so = os.path.join(ROOT, "tools", "variants", f"libzp_{v}.so")
+        l = ctypes.CDLL(so)
+        l.zp_parse_batch_device.restype = ctypes.c_int
+        l.zp_parse_batch_device.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_uint64] + \
+            [ctypes.c_void_p] * 3
+        libs[v] = l
+    sizes = {"c1": 1 << 20, "c2": 1 << 20, "c3": 1 << 24, "c4": 1 << 24, "c5": 1 << 25}
+    if args.membw:
+        mb = ctypes.CDLL(os.path.join(ROOT, "tools", "libmembw.so"))
+        mb.membw_read.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                  ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+        buf = torch.randint(0, 255, (13 << 30,), dtype=torch.uint8, device=dev)
+        out = torch.zeros(1 << 16, dtype=torch.int32, device=dev)
+        for blocks in (2048, 4096, 8192, 16384):
+            for nt in (0, 1):
+                ms = time_launches(lambda: mb.membw_read(buf.data_ptr(), buf.numel(),
+                                                         out.data_ptr(), blocks, nt, None), 10)
+                print(f"membw read 13 GiB blocks={blocks} nt={nt}: "
+                      f"{buf.numel() / (np.median(ms) * 1e-3) / 1e9:.0f} GB/s "
+                      f"(min {min(ms):.3f} ms)", flush=True)
+        del buf
+        torch.cuda.empty_cache()
+    for cfg in args.configs.split(","):
+        n = sizes[cfg]
+        arena, offs, lens = zp.batch.generate(cfg, n, device=dev)
+        rec = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+        ext = torch.zeros((n, 12), dtype=torch.uint8, device=dev)
+        nbytes = int(lens.to(torch.int64).sum())
+        ref = None
+        res = {k: [] for k in libs}
+        for r in range(args.rounds):
+            for name, l in libs.items():
+                fn = lambda l=l: l.zp_parse_batch_device(arena.data_ptr(), offs.data_ptr(),
+                                                          lens.data_ptr(), n, rec.data_ptr(),
+                                                          ext.data_ptr(), None)
+                res[name] += time_launches(fn, args.reps)
+                if r == 0:
+                    if ref is None:
+                        ref = rec.clone()
+                    elif not torch.equal(ref, rec):
+                        print(f"  !! {name}: records differ from base on {cfg}", flush=True)
+        for name, ms in res.items():
+            med = float(np.median(ms))
+            print(f"{cfg} {name:>12}: {med:8.3f} ms  {nbytes / med / 1e6:7.0f} GB/s  "
+                  f"{n / med / 1e3:8.0f} Mpkt/s  (min {min(ms):.3f})", flush=True)
+        del arena, offs, lens, rec, ext
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

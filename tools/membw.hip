@@ -1,0 +1,38 @@
+// membw.hip — known-good HBM read ceiling on this box (guide §5.4 rule 10):
+// every byte of a buffer read once with coalesced 16-B loads (plain and
+// nontemporal), grid-stride, one u32 result per block so nothing is DCE'd.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+template <bool NT>
+__global__ void __launch_bounds__(256) read_sum(const uint4* __restrict__ p, uint64_t n16,
+                                                uint32_t* __restrict__ out) {
+    uint32_t acc = 0;
+    uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+#pragma unroll 4
+    for (; i < n16; i += stride) {
+        typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4* q = (const u32x4*)(p + i);
+        u32x4 v = NT ? __builtin_nontemporal_load(q) : *q;
+        acc += v.x ^ v.y ^ v.z ^ v.w;
+    }
+    __shared__ uint32_t s[256];
+    s[threadIdx.x] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t a = 0;
+        for (int k = 0; k < 256; ++k) a += s[k];
+        out[blockIdx.x] = a;
+    }
+}
+
+extern "C" int membw_read(const void* p, uint64_t bytes, uint32_t* out, int blocks, int nt,
+                          void* stream) {
+    uint64_t n16 = bytes / 16;
+    if (nt) hipLaunchKernelGGL(read_sum<true>, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                               (const uint4*)p, n16, out);
+    else hipLaunchKernelGGL(read_sum<false>, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                            (const uint4*)p, n16, out);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}

@@ -55,18 +55,18 @@ struct zp_ctx {
 extern "C" void zp_ctx_destroy(zp_ctx* c) {
     if (!c) return;
     int prev = 0;
-    hipGetDevice(&prev);
-    hipSetDevice(c->device);
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(c->device);
     for (int k = 0; k < SLOTS; ++k) {
-        if (c->s[k]) hipStreamSynchronize(c->s[k]);
-        hipFree(c->d_arena[k]); hipFree(c->d_offs[k]); hipFree(c->d_lens[k]);
-        hipFree(c->d_rec[k]); hipFree(c->d_ext[k]);
-        hipHostFree(c->h_arena[k]); hipHostFree(c->h_offs[k]); hipHostFree(c->h_lens[k]);
-        hipHostFree(c->h_rec[k]); hipHostFree(c->h_ext[k]);
-        if (c->ev[k]) hipEventDestroy(c->ev[k]);
-        if (c->s[k]) hipStreamDestroy(c->s[k]);
+        if (c->s[k]) (void)hipStreamSynchronize(c->s[k]);
+        (void)hipFree(c->d_arena[k]); (void)hipFree(c->d_offs[k]); (void)hipFree(c->d_lens[k]);
+        (void)hipFree(c->d_rec[k]); (void)hipFree(c->d_ext[k]);
+        (void)hipHostFree(c->h_arena[k]); (void)hipHostFree(c->h_offs[k]); (void)hipHostFree(c->h_lens[k]);
+        (void)hipHostFree(c->h_rec[k]); (void)hipHostFree(c->h_ext[k]);
+        if (c->ev[k]) (void)hipEventDestroy(c->ev[k]);
+        if (c->s[k]) (void)hipStreamDestroy(c->s[k]);
     }
-    hipSetDevice(prev);
+    (void)hipSetDevice(prev);
     free(c);
 }
 
@@ -79,7 +79,7 @@ extern "C" zp_ctx* zp_ctx_create(int device, uint64_t chunk_bytes) {
     c->device = device;
     c->chunk_bytes = chunk_bytes;
     c->chunk_pkts = chunk_bytes / 64 + 1;
-    hipGetDevice(&prev);
+    (void)hipGetDevice(&prev);
     TRY(hipSetDevice(device));
     for (int k = 0; k < SLOTS; ++k) {
         TRY(hipStreamCreateWithFlags(&c->s[k], hipStreamNonBlocking));
@@ -95,10 +95,10 @@ extern "C" zp_ctx* zp_ctx_create(int device, uint64_t chunk_bytes) {
         TRY(hipHostMalloc(&c->h_rec[k], c->chunk_pkts * sizeof(zp_record), hipHostMallocDefault));
         TRY(hipHostMalloc(&c->h_ext[k], c->chunk_pkts * sizeof(zp_ext_offsets), hipHostMallocDefault));
     }
-    hipSetDevice(prev);
+    (void)hipSetDevice(prev);
     return c;
 fail:
-    hipSetDevice(prev);
+    (void)hipSetDevice(prev);
     zp_ctx_destroy(c);
     return NULL;
 }
@@ -141,7 +141,7 @@ extern "C" int zp_parse_batch_host(zp_ctx* c, const uint8_t* arena, uint64_t are
     if (n == 0) return 0;
     int prev = 0;
     int rc = 0;
-    hipGetDevice(&prev);
+    (void)hipGetDevice(&prev);
     if (hipSetDevice(c->device) != hipSuccess) return -2;
     const bool arena_direct = is_pinned(arena);
     const bool rec_direct = is_pinned(recs);
@@ -180,20 +180,27 @@ extern "C" int zp_parse_batch_host(zp_ctx* c, const uint8_t* arena, uint64_t are
         const uint8_t* src = arena + lo;
         if (!arena_direct) { memcpy(c->h_arena[k], src, hi - lo); src = c->h_arena[k]; }
         hipStream_t s = c->s[k];
-        hipMemcpyAsync(c->d_arena[k], src, hi - lo, hipMemcpyHostToDevice, s);
-        hipMemcpyAsync(c->d_offs[k], c->h_offs[k], m * 8, hipMemcpyHostToDevice, s);
-        hipMemcpyAsync(c->d_lens[k], c->h_lens[k], m * 4, hipMemcpyHostToDevice, s);
+        hipError_t e = hipMemcpyAsync(c->d_arena[k], src, hi - lo, hipMemcpyHostToDevice, s);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(c->d_offs[k], c->h_offs[k], m * 8, hipMemcpyHostToDevice, s);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(c->d_lens[k], c->h_lens[k], m * 4, hipMemcpyHostToDevice, s);
+        if (e != hipSuccess) {
+            snprintf(g_ctx_error, ERRBUF_LEN, "H2D copy: %s", hipGetErrorString(e));
+            rc = -2;
+            break;
+        }
         rc = zp_parse_batch_device(c->d_arena[k], c->d_offs[k], c->d_lens[k], m, c->d_rec[k],
                                    ext ? c->d_ext[k] : NULL, s);
         if (rc) break;
-        hipMemcpyAsync(rec_direct ? (void*)(recs + i) : (void*)c->h_rec[k], c->d_rec[k],
-                       m * sizeof(zp_record), hipMemcpyDeviceToHost, s);
-        if (ext)
-            hipMemcpyAsync(c->h_ext[k], c->d_ext[k], m * sizeof(zp_ext_offsets),
-                           hipMemcpyDeviceToHost, s);
-        hipError_t e = hipEventRecord(c->ev[k], s);
+        e = hipMemcpyAsync(rec_direct ? (void*)(recs + i) : (void*)c->h_rec[k], c->d_rec[k],
+                           m * sizeof(zp_record), hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess && ext)
+            e = hipMemcpyAsync(c->h_ext[k], c->d_ext[k], m * sizeof(zp_ext_offsets),
+                               hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipEventRecord(c->ev[k], s);
         if (e != hipSuccess) {
-            snprintf(g_ctx_error, ERRBUF_LEN, "hipEventRecord: %s", hipGetErrorString(e));
+            snprintf(g_ctx_error, ERRBUF_LEN, "D2H copy / event: %s", hipGetErrorString(e));
             rc = -2;
             break;
         }
@@ -205,7 +212,7 @@ extern "C" int zp_parse_batch_host(zp_ctx* c, const uint8_t* arena, uint64_t are
         int r2 = drain(c, (k + q) % SLOTS, pd[(k + q) % SLOTS], recs, ext, rec_direct);
         if (!rc) rc = r2;
     }
-    hipSetDevice(prev);
+    (void)hipSetDevice(prev);
     return rc;
 }
 

@@ -44,12 +44,14 @@
 #include "../../include/zero_packet.h"
 #include "zp_errstr.h"
 
-#define ZP_TILE 256          // frames per workgroup (= threads)
 #define ZP_WIN 128           // window bytes per frame
 #define ZP_WIN_DW (ZP_WIN / 4)
 #define ZP_WIN_CH (ZP_WIN / 16)
 #define ZP_GIANT 65536u      // segments longer than this take the exact path
-#define ZP_UNROLL 4          // stream blocks in flight per wave
+// Timing-only ablations (tools/build_variants.sh); never set in the product:
+//   ZP_ABL_WIN_OFF   skip the window load
+//   ZP_ABL_FAKE_WALK replace the walk by "pending L4 at offset 42"
+//   ZP_ABL_STREAM_OFF skip the stream loads
 
 static __thread char g_last_error[256];
 
@@ -107,17 +109,25 @@ __device__ __forceinline__ bool csum_ok(uint32_t acc, uint32_t V, bool odd) {
 
 // View of one frame: LDS window column + global fallback.
 struct FrameView {
-    const uint32_t* col;     // &win[0][slot]; dword d at col[d * ZP_TILE]
+    const uint32_t* col;     // &win[wave][0][0]; see win_dw()
+    uint32_t lane;
     const uint8_t* g;        // frame in global memory
     uint32_t shift;          // frame address & 15 (window starts 16-aligned)
     uint32_t wlen;           // frame bytes available in the window
     uint32_t len;            // frame length
 };
 
+// Window dword d of frame `lane` lives at win[d][lane ^ 4*(d/4)]: the XOR
+// keeps both the cooperative chunk writes (8 frames x 8 chunks per
+// instruction) and the per-lane reads conflict-free.
+__device__ __forceinline__ uint32_t win_dw(const FrameView& f, uint32_t d) {
+    return f.col[d * 64 + (f.lane ^ ((d >> 2) << 2))];
+}
+
 __device__ __forceinline__ uint32_t rd8(const FrameView& f, uint32_t x) {
     if (x < f.wlen) {
         uint32_t y = x + f.shift;
-        return (f.col[(y >> 2) * ZP_TILE] >> ((y & 3) * 8)) & 0xFFu;
+        return (win_dw(f, y >> 2) >> ((y & 3) * 8)) & 0xFFu;
     }
     return f.g[x];
 }
@@ -132,7 +142,7 @@ __device__ uint32_t sumV(const FrameView& f, uint32_t lo, uint32_t hi) {
     if (lo < h1) {
         int ylo = (int)(lo + f.shift), yhi = (int)(h1 + f.shift);
         for (int d = ylo >> 2; d <= (yhi - 1) >> 2; ++d)
-            s = sad16(f.col[d * ZP_TILE] & byte_mask(d * 4, ylo, yhi), s);
+            s = sad16(win_dw(f, d) & byte_mask(d * 4, ylo, yhi), s);
     }
     uint32_t l2 = lo > f.wlen ? lo : f.wlen;
     if (l2 < hi) {
@@ -353,186 +363,234 @@ done:
 }
 
 // --------------------------------------------------------------------------
-// The batch kernel.
+// The batch kernel. Every wave is independent: it owns 64 consecutive frames
+// (lane j = frame j), so no workgroup barrier is ever needed; a workgroup is
+// just 4 waves packed for occupancy.
 // --------------------------------------------------------------------------
-struct __align__(16) TileShared {
-    uint32_t win[ZP_WIN_DW][ZP_TILE];   // 32 KiB, dword-column-major windows
-    uint64_t seg_base[ZP_TILE];         // 16-aligned address of the first stream chunk
-    uint32_t seg_lo[ZP_TILE];           // first valid byte in the first chunk
-    uint32_t seg_hi[ZP_TILE];           // end byte relative to seg_base
-    uint32_t pre[ZP_TILE + 1];          // exclusive scan of chunk counts
-    uint32_t acc[ZP_TILE];              // streamed V partial sums
-    uint32_t wsum[ZP_TILE / 64];
-};
 
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        uint32_t t = __shfl_up(v, d, 64);
-        if (lane >= d) v += t;
-    }
-    return v;
+// Wave-wide sum with DPP (row_shr 1/2/4/8 + row_bcast 15/31 inclusive scan,
+// lane 63 holds the total); returns the wave-uniform total.
+__device__ __forceinline__ uint32_t wave_total(uint32_t v) {
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xF, 0xF, true);   // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xF, 0xF, true);   // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xF, 0xF, true);   // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xF, 0xF, true);   // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xC, 0xF, false);  // row_bcast:31
+    return __builtin_amdgcn_readlane(v, 63);
 }
 
-__global__ void __launch_bounds__(ZP_TILE)
+__device__ __forceinline__ uint32_t rdl(uint32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
+
+typedef unsigned zp_u32x4 __attribute__((ext_vector_type(4)));
+
+// Streamed 16-B chunk, read once: nontemporal.
+__device__ __forceinline__ uint4 ld_stream(uintptr_t a) {
+    zp_u32x4 v = __builtin_nontemporal_load((const zp_u32x4*)a);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+// V-sum of bytes [l, h) of a 16-B chunk (l in [0,16), h in (0,16]).
+__device__ __forceinline__ uint32_t chunk_sum(uint4 v, int l, int h, uint32_t s) {
+    if (l == 0 && h == 16) {
+        s = sad16(v.x, s); s = sad16(v.y, s); s = sad16(v.z, s); s = sad16(v.w, s);
+    } else {
+        s = sad16(v.x & byte_mask(0, l, h), s);
+        s = sad16(v.y & byte_mask(4, l, h), s);
+        s = sad16(v.z & byte_mask(8, l, h), s);
+        s = sad16(v.w & byte_mask(12, l, h), s);
+    }
+    return s;
+}
+
+#define ZP_WAVES 4
+#ifndef ZP_G
+#define ZP_G 4        // stream items per group; two groups in flight per wave
+#endif
+
+// One stream item = (frame j of the wave, 1 KiB block k of its stream range).
+struct Items {
+    int j[ZP_G];
+    uint32_t k[ZP_G];
+};
+
+// Stream state of a wave: frames with blocks left in the current pass.
+struct Cursor {
+    uint64_t mask;
+    uint32_t pass;
+    bool done;
+};
+
+__device__ __forceinline__ void fill_items(Items& it, Cursor& cur, uint32_t nblk) {
+#pragma unroll
+    for (int q = 0; q < ZP_G; ++q) {
+        if (!cur.done && cur.mask == 0) {
+            ++cur.pass;
+            cur.mask = __ballot(nblk > cur.pass);
+            cur.done = cur.mask == 0;
+        }
+        if (!cur.done) {
+            it.j[q] = __builtin_ctzll(cur.mask);
+            it.k[q] = cur.pass;
+            cur.mask &= cur.mask - 1;
+        } else {
+            it.j[q] = -1;
+            it.k[q] = 0;
+        }
+    }
+}
+
+// Issues the loads of a group: lane l reads chunk 64k + l of frame j.
+__device__ __forceinline__ void issue_items(const Items& it, uint4 (&v)[ZP_G], int lane,
+                                            uint32_t sb_lo, uint32_t sb_hi, uint32_t nch) {
+#pragma unroll
+    for (int q = 0; q < ZP_G; ++q) {
+        v[q] = make_uint4(0, 0, 0, 0);
+        if (it.j[q] >= 0) {
+            const int j = it.j[q];
+            const uint32_t c = it.k[q] * 64u + (uint32_t)lane;
+            const uintptr_t b = ((uintptr_t)rdl(sb_hi, j) << 32) | rdl(sb_lo, j);
+#ifndef ZP_ABL_STREAM_OFF
+            if (c < rdl(nch, j)) v[q] = ld_stream(b + 16ull * c);
+#endif
+        }
+    }
+}
+
+// Sums a landed group (full chunks only; lanes past the frame hold zeros)
+// and adds each item's total to its frame's lane.
+__device__ __forceinline__ void process_items(const Items& it, const uint4 (&v)[ZP_G], int lane,
+                                              uint32_t& vsum) {
+#pragma unroll
+    for (int q = 0; q < ZP_G; ++q) {
+        if (it.j[q] < 0) break;
+        uint32_t part = sad16(v[q].x, 0u);
+        part = sad16(v[q].y, part);
+        part = sad16(v[q].z, part);
+        part = sad16(v[q].w, part);
+        const uint32_t tot = wave_total(part);
+        if (lane == it.j[q]) vsum += tot;
+    }
+}
+
+#ifdef ZP_MINW
+__global__ void __launch_bounds__(64 * ZP_WAVES, ZP_MINW)
+#else
+__global__ void __launch_bounds__(64 * ZP_WAVES)
+#endif
 zp_parse_kernel(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs,
                 const uint32_t* __restrict__ lens, uint64_t n,
                 zp_record* __restrict__ records, zp_ext_offsets* __restrict__ inner_ext) {
-    __shared__ TileShared sh;
-    const int t = threadIdx.x;
-    const int lane = t & 63;
-    const int wid = t >> 6;
-    const uint64_t p0 = (uint64_t)blockIdx.x * ZP_TILE;
-    const uint64_t p = p0 + t;
+    // Per-wave LDS windows, dword-column-major: win[wave][dword][frame].
+    __shared__ uint32_t win[ZP_WAVES][ZP_WIN_DW][64];
+    const int lane = threadIdx.x & 63;
+    const int wid = threadIdx.x >> 6;
+    const uint64_t f0 = ((uint64_t)blockIdx.x * ZP_WAVES + wid) * 64;
+    if (f0 >= n) return;                       // whole wave past the batch (uniform)
+    const uint64_t p = f0 + lane;
     const bool live = p < n;
+    const uint32_t len = live ? lens[p] : 0;
+    const uint8_t* g = arena + (live ? offs[p] : 0);
+    const uintptr_t ga = (uintptr_t)g;
+    uint32_t* wcol = &win[wid][0][0];
 
-    // ---- descriptors
-    uint64_t off = live ? offs[p] : 0;
-    uint32_t len = live ? lens[p] : 0;
-    const uint8_t* g = arena + off;
-
-    // ---- A. cooperative window load: item j -> frame j / 8, chunk j % 8.
-    // Descriptors go through LDS (seg_base / seg_hi are free until phase C).
-    sh.seg_base[t] = (uint64_t)(uintptr_t)g;
-    sh.seg_hi[t] = len;
-    __syncthreads();
+    // ---- A. window load: instruction k covers frames 8k..8k+7, 8 lanes each
+    // (128 contiguous bytes per frame), registers -> LDS columns.
+#ifndef ZP_ABL_WIN_OFF
+    {
+        const uint32_t alo = (uint32_t)ga, ahi = (uint32_t)(ga >> 32);
 #pragma unroll
-    for (int k = 0; k < ZP_WIN_CH; ++k) {
-        int j = k * ZP_TILE + t;
-        int fr = j / ZP_WIN_CH, ch = j % ZP_WIN_CH;
-        {
-            uint32_t fl = sh.seg_hi[fr];                  // 0 for frames past n
-            uintptr_t fa = (uintptr_t)sh.seg_base[fr];
-            uintptr_t ca = (fa & ~(uintptr_t)15) + 16u * ch;
+        for (int k = 0; k < ZP_WIN_CH; ++k) {
+            const int fr = k * 8 + (lane >> 3), ch = lane & 7;
+            const uint32_t fl = __shfl(len, fr, 64);
+            const uintptr_t fa = ((uintptr_t)(uint32_t)__shfl(ahi, fr, 64) << 32) |
+                                 (uint32_t)__shfl(alo, fr, 64);
+            const uintptr_t ca = (fa & ~(uintptr_t)15) + 16u * ch;
             if (fl >= 64 && ca < fa + fl) {
                 uint4 v = *(const uint4*)ca;
-                sh.win[ch * 4 + 0][fr] = v.x;
-                sh.win[ch * 4 + 1][fr] = v.y;
-                sh.win[ch * 4 + 2][fr] = v.z;
-                sh.win[ch * 4 + 3][fr] = v.w;
+                const int col = fr ^ (ch << 2);
+                wcol[(ch * 4 + 0) * 64 + col] = v.x;
+                wcol[(ch * 4 + 1) * 64 + col] = v.y;
+                wcol[(ch * 4 + 2) * 64 + col] = v.z;
+                wcol[(ch * 4 + 3) * 64 + col] = v.w;
             }
         }
     }
-    __syncthreads();
+#endif
 
-    // ---- B. walk
-    FrameView fv;
-    fv.col = &sh.win[0][t];
-    fv.g = g;
-    fv.shift = (uint32_t)((uintptr_t)g & 15);
-    fv.len = len;
-    {
-        uint32_t avail = ZP_WIN - fv.shift;
-        fv.wlen = len < avail ? len : avail;
+    // ---- Stream range, fixed BEFORE the walk. Past the window the frame is
+    // 16-B aligned (the window ends at its 16-aligned base + 128), so the
+    // stream is the full chunks [wend, ea & ~15); the partial tail chunk is
+    // summed by the frame's own lane. Frames of 64 B..64 KiB only; the walk
+    // later corrects for an L4 start on either side of the window end.
+    const uint32_t shift = (uint32_t)(ga & 15);
+    const uint32_t wlen = len < ZP_WIN - shift ? len : ZP_WIN - shift;
+    const bool giant = len > ZP_GIANT;
+    uint32_t nch = 0;
+    uintptr_t sbase = 0;
+    uint4 tail = make_uint4(0, 0, 0, 0);
+    uint32_t tail_n = 0;                     // valid bytes in the tail chunk
+    if (len >= 64 && !giant && wlen < len) {
+        const uintptr_t ea = ga + len;
+        sbase = ga + wlen;                   // 16-aligned
+        nch = (uint32_t)(((ea & ~(uintptr_t)15) - sbase) >> 4);
+        tail_n = (uint32_t)(ea & 15);
+        if (tail_n) tail = *(const uint4*)(ea & ~(uintptr_t)15);
     }
+    const uint32_t nblk = (nch + 63) >> 6;
+    const uint32_t sb_lo = (uint32_t)sbase, sb_hi = (uint32_t)(sbase >> 32);
+    Cursor cur;
+    cur.mask = __ballot(nblk > 0);
+    cur.pass = 0;
+    cur.done = cur.mask == 0;
+    Items ia, ib;
+    uint4 va[ZP_G], vb[ZP_G];
+    fill_items(ia, cur, nblk);
+    issue_items(ia, va, lane, sb_lo, sb_hi, nch);      // in flight during the walk
+
+    // LDS written by other lanes of this wave: order the wave's LDS ops.
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+    // ---- B. walk (lane per frame)
+    FrameView fv;
+    fv.col = wcol;
+    fv.lane = (uint32_t)lane;
+    fv.g = g;
+    fv.shift = shift;
+    fv.len = len;
+    fv.wlen = wlen;
     Walk w;
     w.rec = zp_record{};
     w.inner = zp_ext_offsets{};
+#ifdef ZP_ABL_FAKE_WALK
+    w.pending = live && len >= 64;
+    w.l4 = 42; w.acc = 0; w.v6 = 0;
+    w.rec.flags = ZP_F_ETHERNET;
+#else
     if (live) walk_frame(fv, w);
     else w.pending = 0;
-
-    // Checksum job: window part now, stream part [S, len) later.
-    uint32_t vwin = 0, nchunks = 0;
-    bool giant = false;
-    if (w.pending) {
-        if (len - w.l4 > ZP_GIANT) {
-            giant = true;
-        } else {
-            uint32_t wend = len < fv.wlen ? len : fv.wlen;
-            if (w.l4 < wend) vwin = sumV(fv, w.l4, wend);
-            uint32_t S = w.l4 > fv.wlen ? w.l4 : fv.wlen;
-            if (S < len) {
-                uintptr_t sa = (uintptr_t)g + S, ea = (uintptr_t)g + len;
-                uintptr_t base = sa & ~(uintptr_t)15;
-                nchunks = (uint32_t)((ea - base + 15) >> 4);
-                sh.seg_base[t] = base;
-                sh.seg_lo[t] = (uint32_t)(sa - base);
-                sh.seg_hi[t] = (uint32_t)(ea - base);
-            }
-        }
+#endif
+    // L4 bytes inside the window and in the tail chunk, minus header bytes
+    // the stream covers.
+    uint32_t vsum = 0, vsub = 0;
+    if (w.pending && !giant) {
+        if (w.l4 < wlen) vsum = sumV(fv, w.l4, wlen);
+        else if (w.l4 > wlen) vsub = sumV(fv, wlen, w.l4);
+        if (tail_n) vsum = chunk_sum(tail, 0, (int)tail_n, vsum);
     }
-    sh.acc[t] = 0;
 
-    // Block exclusive scan of chunk counts.
-    uint32_t inc = wave_incl_scan(nchunks, lane);
-    if (lane == 63) sh.wsum[wid] = inc;
-    __syncthreads();
-    uint32_t wbase = 0, total = 0;
-#pragma unroll
-    for (int k = 0; k < ZP_TILE / 64; ++k) {
-        uint32_t s = sh.wsum[k];
-        wbase += k < wid ? s : 0;
-        total += s;
+    // ---- C. stream: two groups of ZP_G items in flight (ping-pong).
+    while (ia.j[0] >= 0) {
+        fill_items(ib, cur, nblk);
+        issue_items(ib, vb, lane, sb_lo, sb_hi, nch);
+        process_items(ia, va, lane, vsum);
+        if (ib.j[0] < 0) break;
+        fill_items(ia, cur, nblk);
+        issue_items(ia, va, lane, sb_lo, sb_hi, nch);
+        process_items(ib, vb, lane, vsum);
     }
-    sh.pre[t] = wbase + inc - nchunks;
-    if (t == 0) sh.pre[ZP_TILE] = total;
-    __syncthreads();
-
-    // ---- C. flattened stream over all pending chunks of the tile.
-    {
-        uint32_t cur = 0;   // segment cursor (wave-uniform)
-        for (uint32_t blk0 = (uint32_t)wid * 64; blk0 < total; blk0 += ZP_TILE * ZP_UNROLL) {
-            uint4 v[ZP_UNROLL];
-            int seg[ZP_UNROLL];
-            uint32_t lo[ZP_UNROLL], hi[ZP_UNROLL];
-#pragma unroll
-            for (int u = 0; u < ZP_UNROLL; ++u) {
-                uint32_t kb = blk0 + u * ZP_TILE;       // block start item
-                uint32_t k = kb + lane;
-                seg[u] = -1;
-                v[u] = make_uint4(0, 0, 0, 0);
-                if (kb < total) {
-                    while (sh.pre[cur + 1] <= kb) ++cur;          // first segment of block
-                    int s = cur;
-                    for (int q = cur; q < ZP_TILE && sh.pre[q] < kb + 64; ++q)
-                        if (k >= sh.pre[q]) s = q;
-                    if (k < total) {
-                        seg[u] = s;
-                        uint32_t i = k - sh.pre[s];
-                        lo[u] = sh.seg_lo[s];
-                        hi[u] = sh.seg_hi[s];
-                        lo[u] = lo[u] > 16u * i ? lo[u] - 16u * i : 0u;
-                        hi[u] = hi[u] - 16u * i;          // > 0 for a valid item
-                        v[u] = *(const uint4*)(sh.seg_base[s] + 16ull * i);
-                    }
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < ZP_UNROLL; ++u) {
-                uint32_t kb = blk0 + u * ZP_TILE;
-                if (kb >= total) break;
-                uint32_t s16 = 0;
-                if (seg[u] >= 0) {
-                    int l = (int)lo[u], h = hi[u] > 16u ? 16 : (int)hi[u];
-                    if (l == 0 && h == 16) {
-                        s16 = sad16(v[u].x, s16);
-                        s16 = sad16(v[u].y, s16);
-                        s16 = sad16(v[u].z, s16);
-                        s16 = sad16(v[u].w, s16);
-                    } else {
-                        s16 = sad16(v[u].x & byte_mask(0, l, h), s16);
-                        s16 = sad16(v[u].y & byte_mask(4, l, h), s16);
-                        s16 = sad16(v[u].z & byte_mask(8, l, h), s16);
-                        s16 = sad16(v[u].w & byte_mask(12, l, h), s16);
-                    }
-                }
-                // Segmented reduction: prefix sum + run boundaries.
-                uint32_t ps = wave_incl_scan(s16, lane);
-                int sprev = __shfl_up(seg[u], 1, 64);
-                int snext = __shfl_down(seg[u], 1, 64);
-                bool first = lane == 0 || sprev != seg[u];
-                bool last = lane == 63 || snext != seg[u];
-                uint64_t firsts = __ballot(first);
-                // run start lane for this lane
-                uint64_t below = firsts & ((lane == 63) ? ~0ull : ((2ull << lane) - 1ull));
-                int start = 63 - __builtin_clzll(below);
-                uint32_t before = __shfl(ps, start > 0 ? start - 1 : 0, 64);
-                if (start == 0) before = 0;
-                if (last && seg[u] >= 0) atomicAdd(&sh.acc[seg[u]], ps - before);
-            }
-        }
-    }
-    __syncthreads();
 
     // ---- D. finalize + store
     if (!live) return;
@@ -542,20 +600,19 @@ zp_parse_kernel(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ 
         if (giant) {
             ok = csum_ok_exact(g, w.l4, len, w.acc);
         } else {
-            uint32_t V = vwin + sh.acc[t];
-            bool odd = ((uintptr_t)(g + w.l4)) & 1;
-            ok = csum_ok(w.acc, V, odd);
+            bool odd = (ga + w.l4) & 1;
+            ok = csum_ok(w.acc, vsum - vsub, odd);
         }
         if (!ok) {
             r = zp_record{};
             r.err = (uint8_t)(w.v6 ? ZP_ERR_IPV6_L4_CHECKSUM : ZP_ERR_IPV4_L4_CHECKSUM);
         }
     }
-    uint4 q[2];
-    memcpy(q, &r, sizeof r);
+    uint4 q2[2];
+    memcpy(q2, &r, sizeof r);
     uint4* dst = (uint4*)(records + p);
-    dst[0] = q[0];
-    dst[1] = q[1];
+    dst[0] = q2[0];
+    dst[1] = q2[1];
     if (inner_ext && (r.flags & ZP_F_INNER_EXT)) inner_ext[p] = w.inner;
 }
 
@@ -571,12 +628,12 @@ extern "C" int zp_parse_batch_device(const uint8_t* arena, const uint64_t* offs,
         snprintf(g_last_error, sizeof g_last_error, "zp_parse_batch_device: null pointer");
         return -1;
     }
-    uint64_t blocks = (n + ZP_TILE - 1) / ZP_TILE;
+    uint64_t blocks = (n + 64 * ZP_WAVES - 1) / (64 * ZP_WAVES);
     if (blocks > 0x7FFFFFFFull) {
         snprintf(g_last_error, sizeof g_last_error, "zp_parse_batch_device: batch too large");
         return -1;
     }
-    hipLaunchKernelGGL(zp_parse_kernel, dim3((unsigned)blocks), dim3(ZP_TILE), 0,
+    hipLaunchKernelGGL(zp_parse_kernel, dim3((unsigned)blocks), dim3(64 * ZP_WAVES), 0,
                        (hipStream_t)stream, arena, offs, lens, n, records, inner_ext);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) { set_err("zp_parse_kernel launch", e); return -2; }
