@@ -38,10 +38,11 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--membw", action="store_true")
+    ap.add_argument("--no-base", action="store_true", help="time only --variants (PMC runs)")
     args = ap.parse_args()
     zp = importlib.import_module("zero-packet_amd")
     dev = torch.device("cuda:0")
-    libs = {"base": zp._lib.hip()}
+    libs = {} if args.no_base else {"base": zp._lib.hip()}
     for v in [x for x in args.variants.split(",") if x]:
         so = os.path.join(ROOT, "tools", "variants", f"libzp_{v}.so")
         l = ctypes.CDLL(so)

@@ -7,33 +7,34 @@
 // icmpv4.rs:92-104, icmpv6.rs:89-101) and the checksum primitives
 // (checksum.rs:5-69).
 //
-// Kernel structure (one 256-thread workgroup = one tile of 256 frames):
-//   A. cooperative window load: the first 128 B of every frame of the tile
-//      (16-B aligned chunks, 8 consecutive lanes per frame -> coalesced) into
-//      an LDS window stored dword-column-major: win[dword][frame], so a lane
-//      reading ANY dword of its own frame hits bank (frame % 32): no conflicts.
-//   B. lane-per-frame header walk from LDS (global byte loads only for bytes
-//      past the window): Ethernet/VLAN -> ARP / IPv4 / IPv6 + extension chain
-//      -> IP-in-IP levels -> TCP/UDP/ICMP checks, IPv4 header checksums, the
-//      pseudo-header sum and the L4 bytes that sit inside the window.
-//   C. flattened stream: the remaining L4 bytes of all frames of the tile form
-//      a list of 16-B aligned chunks (exclusive scan of per-frame chunk
-//      counts); lane k of the workgroup loads chunk k, k+256, ... so each wave
-//      reads 1 KiB of mostly contiguous arena per load. A wave-wide prefix sum
-//      plus run boundaries turns per-chunk sums into per-frame sums, added to
-//      LDS accumulators once per (frame, 1 KiB block).
-//   D. finalize: checksum validity from the exact partial sums, record store.
+// Work decomposition. Every wave is independent and owns 64 consecutive
+// frames (lane j = frame j); a workgroup is 4 waves packed for occupancy and
+// never synchronises. Per wave:
+//   A.  one round trip of cooperative, coalesced loads: for each frame the
+//       16-B aligned chunks [A&~15, +256) — chunks 0-7 are the 128-B header
+//       window (-> LDS), chunks 8-15 the "seam" up to the next 128-B line
+//       boundary (summed in registers). One 16-lane DPP row per frame.
+//   A2. the frame's partial last 128-B line (summed), issued together with
+//       the first stream group so both are in flight during the walk.
+//   B.  lane-per-frame header walk from the LDS window.
+//   C.  stream: the frame's full 128-B lines strictly inside it, wave-wide
+//       coalesced loads, ZP_G items per group, two groups in flight.
+//   D.  checksum verdict, 32-B record store.
+// Line ownership: every line a frame shares with a neighbour or with its own
+// window is read in A/A2 (close in time, so the second reader hits L2); C
+// reads lines that belong to one frame only, each exactly once.
 //
 // Checksum arithmetic. The reference verifies S = acc + sum of big-endian
 // 16-bit words (u32), valid iff !fold(S) as u16 == 0 (checksum.rs:5-35),
 // i.e. S != 0 and S == 0 (mod 65535). We sum little-endian 16-bit words at
 // even ARENA addresses (V = E + 256*O, E/O = sums of bytes at even/odd
-// addresses) because that is what aligned dword loads give for free:
+// addresses) because that is what aligned loads give for free:
 //   segment starting at an odd address:  W = V exactly,
 //   segment starting at an even address: W == 256*V (mod 65535),
-// and W == 0 iff V == 0. Exact u32 sums hold for segments <= 64 KiB; longer
-// (IPv6 jumbo) segments take an exact E/O path that reproduces the
-// reference's u32 wrap-around.
+// and W == 0 iff V == 0. Exact u32 sums hold for frames <= 64 KiB; longer
+// (IPv6 jumbo) frames take an exact E/O path that reproduces the reference's
+// u32 wrap-around. The pseudo-header accumulator is computed exactly from
+// E/O sums of the address bytes.
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -45,13 +46,16 @@
 #include "zp_errstr.h"
 
 #define ZP_WIN 128           // window bytes per frame
-#define ZP_WIN_DW (ZP_WIN / 4)
 #define ZP_WIN_CH (ZP_WIN / 16)
-#define ZP_GIANT 65536u      // segments longer than this take the exact path
+#define ZP_GIANT 65536u      // frames longer than this take the exact path
+#define ZP_WAVES 4           // waves per workgroup
+#ifndef ZP_G
+#define ZP_G 8               // stream items (1 KiB loads) per group
+#endif
 // Timing-only ablations (tools/build_variants.sh); never set in the product:
-//   ZP_ABL_WIN_OFF   skip the window load
-//   ZP_ABL_FAKE_WALK replace the walk by "pending L4 at offset 42"
+//   ZP_ABL_FAKE_WALK  replace the walk by "pending L4 at offset 42"
 //   ZP_ABL_STREAM_OFF skip the stream loads
+//   ZP_STAMPS         per-wave phase timestamps (tools/stamps.py)
 
 static __thread char g_last_error[256];
 
@@ -68,8 +72,7 @@ extern "C" const char* zp_err_str(int code) { return zp_err_string(code); }
 // Device helpers
 // --------------------------------------------------------------------------
 
-// Valid ICMPv4 types (misc.rs:93-119) / ICMPv6 types (misc.rs:164-204) as
-// 256-bit sets.
+// Valid ICMPv4 types (misc.rs:93-119) / ICMPv6 types (misc.rs:164-204).
 __device__ __forceinline__ bool icmpv4_type_ok(uint32_t t) {
     const uint64_t m0 = (1ull << 0) | (1ull << 3) | (1ull << 4) | (1ull << 5) | (1ull << 8) |
                         (1ull << 9) | (1ull << 10) | (1ull << 11) | (1ull << 12) | (1ull << 13) |
@@ -83,6 +86,45 @@ __device__ __forceinline__ bool icmpv6_type_ok(uint32_t t) {
     if (t == 100 || t == 101 || t == 155 || t == 200 || t == 201) return true;
     return t >= 128 && t <= 153;
 }
+
+// All loads go through address_space(1) pointers: pointers rebuilt from
+// integers would otherwise compile to FLAT loads, which count against both
+// vmcnt and lgkmcnt, so every LDS wait would also drain in-flight HBM loads.
+#define ZP_GLOBAL __attribute__((address_space(1)))
+typedef unsigned zp_u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint4 ldg16(uintptr_t a) {
+    zp_u32x4 v = *(const ZP_GLOBAL zp_u32x4*)a;
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint32_t ldg4(uintptr_t a) { return *(const ZP_GLOBAL uint32_t*)a; }
+__device__ __forceinline__ uint32_t ldg1(uintptr_t a) { return *(const ZP_GLOBAL uint8_t*)a; }
+
+// Streamed 16-B chunk, read once: nontemporal.
+__device__ __forceinline__ uint4 ld_stream(uintptr_t a) {
+    zp_u32x4 v = __builtin_nontemporal_load((const ZP_GLOBAL zp_u32x4*)a);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+// A readable 16-B chunk for masked lanes of frames that own no bytes.
+__device__ uint4 zp_safe_chunk;
+
+// Diagnostic build only (-DZP_STAMPS): per-wave s_memrealtime stamps at the
+// phase boundaries, written to their own buffer (never read by the kernel).
+#ifdef ZP_STAMPS
+#define ZP_NSTAMP 8
+__device__ unsigned long long* zp_stamp_buf;
+#define STAMP(i)                                                               \
+    do {                                                                       \
+        unsigned long long t_ = __builtin_amdgcn_s_memrealtime();              \
+        if (zp_stamp_buf && lane == 0) zp_stamp_buf[wave_id * ZP_NSTAMP + (i)] = t_; \
+    } while (0)
+extern "C" int zp_stamps_set(void* p) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(zp_stamp_buf), &p, sizeof p) == hipSuccess ? 0 : -1;
+}
+#else
+#define STAMP(i) do {} while (0)
+#endif
 
 // Keep bytes [lo, hi) of the dword whose first byte is at position `base`.
 __device__ __forceinline__ uint32_t byte_mask(int base, int lo, int hi) {
@@ -98,6 +140,19 @@ __device__ __forceinline__ uint32_t sad16(uint32_t x, uint32_t acc) {
     return __builtin_amdgcn_sad_u16(x, 0u, acc);
 }
 
+// V-sum of bytes [l, h) of a 16-B chunk (0 <= l < h <= 16).
+__device__ __forceinline__ uint32_t chunk_sum(uint4 v, int l, int h, uint32_t s) {
+    if (l == 0 && h == 16) {
+        s = sad16(v.x, s); s = sad16(v.y, s); s = sad16(v.z, s); s = sad16(v.w, s);
+    } else {
+        s = sad16(v.x & byte_mask(0, l, h), s);
+        s = sad16(v.y & byte_mask(4, l, h), s);
+        s = sad16(v.z & byte_mask(8, l, h), s);
+        s = sad16(v.w & byte_mask(12, l, h), s);
+    }
+    return s;
+}
+
 // Checksum validity from the arena-parity sum V of a segment starting at an
 // address of parity `odd`, with accumulator acc (fast path, exact V).
 __device__ __forceinline__ bool csum_ok(uint32_t acc, uint32_t V, bool odd) {
@@ -107,21 +162,26 @@ __device__ __forceinline__ bool csum_ok(uint32_t acc, uint32_t V, bool odd) {
     return ((acc % 65535u) + w) % 65535u == 0;
 }
 
-// View of one frame: LDS window column + global fallback.
+// --------------------------------------------------------------------------
+// Frame view: LDS window (16-B cells, chunk c of frame f at win[c][f ^ c]:
+// conflict-free for the cooperative ds_write_b128 of phase A and for each
+// lane's ds_read_b128 of its own frame) + global fallback past the window.
+// --------------------------------------------------------------------------
 struct FrameView {
-    const uint32_t* col;     // &win[wave][0][0]; see win_dw()
-    uint32_t lane;
+    const uint4* win;        // this wave's window, [ZP_WIN_CH][64]
     const uint8_t* g;        // frame in global memory
+    uint32_t lane;
     uint32_t shift;          // frame address & 15 (window starts 16-aligned)
     uint32_t wlen;           // frame bytes available in the window
     uint32_t len;            // frame length
 };
 
-// Window dword d of frame `lane` lives at win[d][lane ^ 4*(d/4)]: the XOR
-// keeps both the cooperative chunk writes (8 frames x 8 chunks per
-// instruction) and the per-lane reads conflict-free.
+__device__ __forceinline__ uint4 win_chunk(const FrameView& f, uint32_t c) {
+    return f.win[c * 64 + (f.lane ^ c)];
+}
 __device__ __forceinline__ uint32_t win_dw(const FrameView& f, uint32_t d) {
-    return f.col[d * 64 + (f.lane ^ ((d >> 2) << 2))];
+    const uint32_t c = d >> 2;
+    return ((const uint32_t*)&f.win[c * 64 + (f.lane ^ c)])[d & 3];
 }
 
 __device__ __forceinline__ uint32_t rd8(const FrameView& f, uint32_t x) {
@@ -129,41 +189,84 @@ __device__ __forceinline__ uint32_t rd8(const FrameView& f, uint32_t x) {
         uint32_t y = x + f.shift;
         return (win_dw(f, y >> 2) >> ((y & 3) * 8)) & 0xFFu;
     }
-    return f.g[x];
+    return ldg1((uintptr_t)f.g + x);
 }
+
+// Big-endian 16-bit field at frame offset x.
 __device__ __forceinline__ uint32_t rd16(const FrameView& f, uint32_t x) {
+    if (x + 1 < f.wlen) {
+        const uint32_t y = x + f.shift, d = y >> 2;
+        const uint32_t lo = win_dw(f, d);
+        const uint32_t hi = (y & 3) == 3 ? win_dw(f, d + 1) : 0u;
+        const uint32_t t = __builtin_amdgcn_alignbyte(hi, lo, y & 3);
+        return ((t & 0xFFu) << 8) | ((t >> 8) & 0xFFu);
+    }
     return (rd8(f, x) << 8) | rd8(f, x + 1);
 }
 
 // Arena-parity word sum V of frame bytes [lo, hi) (both <= len).
 __device__ uint32_t sumV(const FrameView& f, uint32_t lo, uint32_t hi) {
     uint32_t s = 0;
-    uint32_t h1 = hi < f.wlen ? hi : f.wlen;
+    const uint32_t h1 = hi < f.wlen ? hi : f.wlen;
     if (lo < h1) {
-        int ylo = (int)(lo + f.shift), yhi = (int)(h1 + f.shift);
-        for (int d = ylo >> 2; d <= (yhi - 1) >> 2; ++d)
-            s = sad16(win_dw(f, d) & byte_mask(d * 4, ylo, yhi), s);
+        const int ylo = (int)(lo + f.shift), yhi = (int)(h1 + f.shift);
+        const int c0 = ylo >> 4, c1 = (yhi - 1) >> 4;
+        for (int c = c0; c <= c1; ++c) {
+            const int l = c == c0 ? ylo - 16 * c : 0;
+            const int h = c == c1 ? yhi - 16 * c : 16;
+            s = chunk_sum(win_chunk(f, c), l, h, s);
+        }
     }
-    uint32_t l2 = lo > f.wlen ? lo : f.wlen;
+    const uint32_t l2 = lo > f.wlen ? lo : f.wlen;
     if (l2 < hi) {
-        uintptr_t a0 = (uintptr_t)f.g + l2, a1 = (uintptr_t)f.g + hi;
+        const uintptr_t a0 = (uintptr_t)f.g + l2, a1 = (uintptr_t)f.g + hi;
         for (uintptr_t d = a0 & ~(uintptr_t)3; d < a1; d += 4) {
-            uint32_t v = *(const uint32_t*)d;
-            s = sad16(v & byte_mask(0, (int)((intptr_t)a0 - (intptr_t)d),
-                                    (int)((intptr_t)a1 - (intptr_t)d)), s);
+            const int l = a0 > d ? (int)(a0 - d) : 0;
+            const int h = a1 - d < 4 ? (int)(a1 - d) : 4;
+            s = sad16(ldg4(d) & byte_mask(0, l, h), s);
         }
     }
     return s;
+}
+
+// V-sum of the bytes [A & ~15, A) that precede the frame in its first chunk.
+__device__ __forceinline__ uint32_t sum_head(const FrameView& f) {
+    return f.shift ? chunk_sum(win_chunk(f, 0), 0, (int)f.shift, 0u) : 0u;
+}
+
+// Exact big-endian word sum (reference parity: words start at lo) of frame
+// bytes [lo, hi): split into even/odd-offset byte sums.
+__device__ uint32_t sumW_exact(const FrameView& f, uint32_t lo, uint32_t hi) {
+    uint32_t E = 0, O = 0;
+    for (uint32_t x = lo; x < hi; x += 4) {
+        uint32_t v;
+        const int n = (int)(hi - x) < 4 ? (int)(hi - x) : 4;
+        if (x + 3 < f.wlen) {
+            const uint32_t y = x + f.shift, d = y >> 2;
+            const uint32_t a = win_dw(f, d);
+            const uint32_t b = (y & 3) ? win_dw(f, d + 1) : 0u;
+            v = __builtin_amdgcn_alignbyte(b, a, y & 3);
+        } else {
+            v = 0;
+            for (int k = 0; k < n; ++k) v |= rd8(f, x + k) << (8 * k);
+        }
+        v &= byte_mask(0, 0, n);
+        // offsets relative to lo: even ones are the high bytes of the words
+        E += (v & 0xFFu) + ((v >> 16) & 0xFFu);
+        O += ((v >> 8) & 0xFFu) + (v >> 24);
+    }
+    return 256u * E + O;
 }
 
 // Exact reference checksum for long segments: sums even/odd-address bytes
 // separately and reproduces the u32 wrap of checksum.rs:12 (release build).
 __device__ bool csum_ok_exact(const uint8_t* g, uint32_t lo, uint32_t hi, uint32_t acc) {
     uint64_t E = 0, O = 0;
-    uintptr_t a0 = (uintptr_t)g + lo, a1 = (uintptr_t)g + hi;
+    const uintptr_t a0 = (uintptr_t)g + lo, a1 = (uintptr_t)g + hi;
     for (uintptr_t d = a0 & ~(uintptr_t)3; d < a1; d += 4) {
-        uint32_t v = *(const uint32_t*)d;
-        v &= byte_mask(0, (int)((intptr_t)a0 - (intptr_t)d), (int)((intptr_t)a1 - (intptr_t)d));
+        const int l = a0 > d ? (int)(a0 - d) : 0;
+        const int h = a1 - d < 4 ? (int)(a1 - d) : 4;
+        uint32_t v = ldg4(d) & byte_mask(0, l, h);
         E += (v & 0xFFu) + ((v >> 16) & 0xFFu);
         O += ((v >> 8) & 0xFFu) + (v >> 24);
     }
@@ -173,11 +276,13 @@ __device__ bool csum_ok_exact(const uint8_t* g, uint32_t lo, uint32_t hi, uint32
     return (uint16_t)~S == 0;
 }
 
-// Per-frame walk result.
+// --------------------------------------------------------------------------
+// The header-chain walk of PacketParser::parse for one frame.
+// --------------------------------------------------------------------------
 struct Walk {
     zp_record rec;
     zp_ext_offsets inner;
-    uint32_t acc;        // pseudo-header accumulator of the innermost IP
+    uint32_t acc;        // exact pseudo-header accumulator of the innermost IP
     uint32_t l4;         // L4 start (frame offset) when a checksum is pending
     uint8_t pending;     // 1 = L4 checksum still to verify
     uint8_t v6;          // innermost IP is IPv6 (selects the error code)
@@ -191,7 +296,7 @@ __device__ int ext_walk(const FrameView& f, uint32_t pos, uint32_t nh,
     uint32_t pres = 0, tot = 0, fin = 0;
     uint32_t cur = nh, p = pos;
     for (int it = 0; it < 8; ++it) {
-        uint32_t rem = f.len - p;
+        const uint32_t rem = f.len - p;
         int slot;
         uint32_t hl;
         if (cur == 0) {                                   // Hop-by-Hop (:90-113)
@@ -227,7 +332,7 @@ __device__ int ext_walk(const FrameView& f, uint32_t pos, uint32_t nh,
         } else {
             break;
         }
-        uint32_t next = rd8(f, p);
+        const uint32_t next = rd8(f, p);
         pres |= 1u << slot;
 #pragma unroll
         for (int k = 0; k < 6; ++k)
@@ -243,7 +348,6 @@ __device__ int ext_walk(const FrameView& f, uint32_t pos, uint32_t nh,
     return 0;
 }
 
-// The header-chain walk of PacketParser::parse for one frame.
 __device__ void walk_frame(const FrameView& f, Walk& w) {
     zp_record& r = w.rec;
     w.pending = 0; w.acc = 0; w.l4 = 0; w.v6 = 0;
@@ -252,14 +356,14 @@ __device__ void walk_frame(const FrameView& f, Walk& w) {
     if (len < 64) { err = ZP_ERR_ETH_FRAME_TOO_SHORT; goto done; }   // parser.rs:159
     {
         uint32_t hl = 14;                                             // ethernet.rs:155-179
-        uint32_t t0 = rd16(f, 12);
+        const uint32_t t0 = rd16(f, 12);
         if (t0 == 0x8100) hl = 18;
         else if (t0 == 0x88A8) {
             if (rd16(f, 16) != 0x8100) { err = ZP_ERR_ETH_INVALID_QINQ; goto done; }
             hl = 22;
         }
         r.eth_len = (uint8_t)hl;
-        uint32_t et = rd16(f, hl - 2);                                 // ethernet.rs:209-212
+        const uint32_t et = rd16(f, hl - 2);                           // ethernet.rs:209-212
         if (et == 0x0806) {                                           // ARP, parser.rs:60,172-180
             if (len - hl < 28) { err = ZP_ERR_ARP_TOO_SHORT; goto done; }
             if (rd16(f, hl + 6) > 2) { err = ZP_ERR_ARP_INVALID_OPER; goto done; }
@@ -268,37 +372,35 @@ __device__ void walk_frame(const FrameView& f, Walk& w) {
             uint32_t pos = hl;
             bool v4 = et == 0x0800;
             for (uint32_t level = 0;; ++level) {
-                uint32_t sl = len - pos;                              // slice length
+                const uint32_t sl = len - pos;                        // slice length
                 uint32_t proto, pp, acc;
                 if (v4) {                                             // parser.rs:188-212
                     if (sl < 20) { err = ZP_ERR_IPV4_TOO_SHORT; goto done; }
-                    uint32_t b0 = rd8(f, pos);
+                    const uint32_t b0 = rd8(f, pos);
                     if ((b0 >> 4) != 4) { err = ZP_ERR_IPV4_VERSION; goto done; }
-                    uint32_t ihl = (b0 & 15) * 4;
+                    const uint32_t ihl = (b0 & 15) * 4;
                     if (ihl < 20) { err = ZP_ERR_IPV4_IHL_TOO_SHORT; goto done; }
                     if (sl < ihl) { err = ZP_ERR_IPV4_HDR_TOO_LONG; goto done; }
                     if (rd16(f, pos + 2) != sl) { err = ZP_ERR_IPV4_TOTAL_LENGTH; goto done; }
-                    uint32_t hv = sumV(f, pos, pos + ihl);             // ipv4.rs:262-264
+                    const uint32_t hv = sumV(f, pos, pos + ihl);       // ipv4.rs:262-264
                     if (!(hv != 0 && hv % 65535u == 0)) { err = ZP_ERR_IPV4_CHECKSUM; goto done; }
                     proto = rd8(f, pos + 9);
                     pp = pos + ihl;
-                    if (proto == 1) acc = 0;                          // parser.rs:322-326
-                    else acc = rd16(f, pos + 12) + rd16(f, pos + 14) + rd16(f, pos + 16) +
-                               rd16(f, pos + 18) + proto + (len - pp);
+                    // parser.rs:322-326: no pseudo-header for ICMPv4
+                    acc = proto == 1 ? 0u : sumW_exact(f, pos + 12, pos + 20) + proto + (len - pp);
                     if (level == 0) r.flags |= ZP_F_IPV4;
                     else if (level == 1) { r.flags |= ZP_F_IP_IN_IP; r.inner_off = pos; }
                 } else {                                              // parser.rs:222-230
                     if (sl < 40) { err = ZP_ERR_IPV6_TOO_SHORT; goto done; }
                     uint32_t pres = 0, tot = 0, fin = 0;
                     uint16_t eo[6] = {0, 0, 0, 0, 0, 0};
-                    uint32_t nh = rd8(f, pos + 6);
-                    int e = ext_walk(f, pos + 40, nh, &pres, eo, &tot, &fin);   // ipv6.rs:159
+                    const uint32_t nh = rd8(f, pos + 6);
+                    const int e = ext_walk(f, pos + 40, nh, &pres, eo, &tot, &fin);  // ipv6.rs:159
                     if (e) { err = e; goto done; }
                     if ((rd8(f, pos) >> 4) != 6) { err = ZP_ERR_IPV6_VERSION; goto done; }
                     proto = pres ? fin : nh;                          // ipv6.rs:219-227
                     pp = pos + 40 + tot;                              // ipv6.rs:283-285
-                    acc = proto + (len - pp);                         // parser.rs:349-354
-                    for (uint32_t k = 0; k < 32; k += 2) acc += rd16(f, pos + 8 + k);
+                    acc = sumW_exact(f, pos + 8, pos + 40) + proto + (len - pp);  // parser.rs:349-354
                     if (level == 0) {
                         r.flags |= ZP_F_IPV6;
                         r.final_nh = (uint8_t)proto;
@@ -318,11 +420,12 @@ __device__ void walk_frame(const FrameView& f, Walk& w) {
                         }
                     }
                 }
-                uint32_t rem = len - pp;                              // parse_protocol :111-140
+                const uint32_t rem = len - pp;                        // parse_protocol :111-140
                 if (proto == 6) {
                     if (rem < 20) { err = ZP_ERR_TCP_TOO_SHORT; goto done; }
-                    if ((rd8(f, pp + 12) >> 4) * 4 < 20) { err = ZP_ERR_TCP_DATA_OFFSET; goto done; }
-                    if (rd8(f, pp + 13) == 0) { err = ZP_ERR_TCP_FLAGS; goto done; }
+                    const uint32_t t = rd16(f, pp + 12);
+                    if ((t >> 12) * 4 < 20) { err = ZP_ERR_TCP_DATA_OFFSET; goto done; }
+                    if ((t & 0xFF) == 0) { err = ZP_ERR_TCP_FLAGS; goto done; }
                     r.flags |= ZP_F_TCP;
                 } else if (proto == 17) {
                     if (rem < 8) { err = ZP_ERR_UDP_TOO_SHORT; goto done; }
@@ -330,8 +433,9 @@ __device__ void walk_frame(const FrameView& f, Walk& w) {
                     r.flags |= ZP_F_UDP;
                 } else if (proto == 1) {
                     if (rem < 8) { err = ZP_ERR_ICMP_TOO_SHORT; goto done; }
-                    if (!icmpv4_type_ok(rd8(f, pp))) { err = ZP_ERR_ICMPV4_TYPE; goto done; }
-                    if (rd8(f, pp + 1) > 15) { err = ZP_ERR_ICMPV4_CODE; goto done; }
+                    const uint32_t t = rd16(f, pp);
+                    if (!icmpv4_type_ok(t >> 8)) { err = ZP_ERR_ICMPV4_TYPE; goto done; }
+                    if ((t & 0xFF) > 15) { err = ZP_ERR_ICMPV4_CODE; goto done; }
                     r.flags |= ZP_F_ICMPV4;
                 } else if (proto == 58) {
                     if (rem < 8) { err = ZP_ERR_ICMP_TOO_SHORT; goto done; }
@@ -363,201 +467,239 @@ done:
 }
 
 // --------------------------------------------------------------------------
-// The batch kernel. Every wave is independent: it owns 64 consecutive frames
-// (lane j = frame j), so no workgroup barrier is ever needed; a workgroup is
-// just 4 waves packed for occupancy.
+// Cross-lane scans (DPP).
 // --------------------------------------------------------------------------
 
-// Wave-wide sum with DPP (row_shr 1/2/4/8 + row_bcast 15/31 inclusive scan,
-// lane 63 holds the total); returns the wave-uniform total.
-__device__ __forceinline__ uint32_t wave_total(uint32_t v) {
+// Inclusive wave-wide prefix sum: row_shr 1/2/4/8 scan each 16-lane row,
+// row_bcast 15/31 carry the row totals upward.
+__device__ __forceinline__ uint32_t wave_scan(uint32_t v) {
     v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xF, 0xF, true);   // row_shr:1
     v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xF, 0xF, true);   // row_shr:2
     v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xF, 0xF, true);   // row_shr:4
     v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xF, 0xF, true);   // row_shr:8
     v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xA, 0xF, false);  // row_bcast:15
     v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xC, 0xF, false);  // row_bcast:31
-    return __builtin_amdgcn_readlane(v, 63);
+    return v;
 }
 
-__device__ __forceinline__ uint32_t rdl(uint32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
-
-typedef unsigned zp_u32x4 __attribute__((ext_vector_type(4)));
-
-// Streamed 16-B chunk, read once: nontemporal.
-__device__ __forceinline__ uint4 ld_stream(uintptr_t a) {
-    zp_u32x4 v = __builtin_nontemporal_load((const zp_u32x4*)a);
-    return make_uint4(v.x, v.y, v.z, v.w);
+__device__ __forceinline__ uint32_t rdl(uint32_t v, uint32_t l) {
+    return __builtin_amdgcn_readlane(v, (int)l);
 }
 
-// V-sum of bytes [l, h) of a 16-B chunk (l in [0,16), h in (0,16]).
-__device__ __forceinline__ uint32_t chunk_sum(uint4 v, int l, int h, uint32_t s) {
-    if (l == 0 && h == 16) {
-        s = sad16(v.x, s); s = sad16(v.y, s); s = sad16(v.z, s); s = sad16(v.w, s);
-    } else {
-        s = sad16(v.x & byte_mask(0, l, h), s);
-        s = sad16(v.y & byte_mask(4, l, h), s);
-        s = sad16(v.z & byte_mask(8, l, h), s);
-        s = sad16(v.w & byte_mask(12, l, h), s);
+// V-sum of bytes [lo, hi) of a 16-B chunk (0 <= lo <= hi <= 16).
+__device__ __forceinline__ uint32_t range_sum(uint4 v, uint32_t lo, uint32_t hi) {
+    uint32_t s = 0;
+    const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int a = (int)lo - 4 * i, b = (int)hi - 4 * i;
+        const uint32_t na = a < 0 ? 0u : (a > 4 ? 4u : (uint32_t)a);
+        const uint32_t nb = b < 0 ? 0u : (b > 4 ? 4u : (uint32_t)b);
+        const uint32_t m = (uint32_t)(0xFFFFFFFFull >> (32u - 8u * nb)) &
+                           ~(uint32_t)(0xFFFFFFFFull >> (32u - 8u * na));
+        s = sad16(d[i] & m, s);
     }
     return s;
 }
 
-#define ZP_WAVES 4
-#ifndef ZP_G
-#define ZP_G 4        // stream items per group; two groups in flight per wave
-#endif
-
-// One stream item = (frame j of the wave, 1 KiB block k of its stream range).
-struct Items {
-    int j[ZP_G];
-    uint32_t k[ZP_G];
+// --------------------------------------------------------------------------
+// The stream. Every byte of a frame is read exactly once, by one wave-wide
+// coalesced stream: the 16-B chunks [A & ~15, E) of the wave's frames are
+// concatenated into one virtual sequence of T chunks (exclusive scan of the
+// per-frame chunk counts) and read in items of 64 chunks, so every load
+// instruction is a full 1 KiB whatever the frame lengths, and the chunks of
+// a 128-B line shared by two neighbouring frames are read by adjacent lanes
+// of the same or the next item (no second HBM fetch).
+//
+// Frames that own chunks are numbered by rank (compaction of the wave's
+// non-empty frames). Lane l of item i reads virtual chunk vv = 64i + l of
+// frame rank r(vv): a scalar loop sets one bit of a 64-bit mask F per frame
+// starting inside the item, and r = (frames started before the item) - 1 +
+// popcount(F & lanes <= l) is one v_mbcnt pair; the frame's address and
+// bounds then come from its rank with ds_bpermute. Per-frame sums need no
+// segmented reduction: with C(vv) the running inclusive sum of the stream,
+// the lane holding a frame's last chunk records C there, and the frame's sum
+// is C(last of r) - C(last of r - 1).
+// The first 8 chunks of each frame (the header window) and its last chunk
+// are also written to LDS for the walk and the verdict.
+// --------------------------------------------------------------------------
+struct Cursor {          // wave-uniform (SGPRs)
+    uint64_t rem;        // ranks whose first chunk is not yet passed (lane mask)
+    uint32_t ns;         // first virtual chunk of the next such frame
+    uint32_t rbase;      // rank of the frame holding the chunk before the item
 };
 
-// Stream state of a wave: frames with blocks left in the current pass.
-struct Cursor {
-    uint64_t mask;
-    uint32_t pass;
-    bool done;
+struct Ranked {          // lane r = frame of rank r
+    uint32_t org_lo, org_hi;   // (A & ~15) - 16 * pfx
+    uint32_t last;       // last virtual chunk
+    uint32_t pfx;        // first virtual chunk
 };
 
-__device__ __forceinline__ void fill_items(Items& it, Cursor& cur, uint32_t nblk) {
-#pragma unroll
-    for (int q = 0; q < ZP_G; ++q) {
-        if (!cur.done && cur.mask == 0) {
-            ++cur.pass;
-            cur.mask = __ballot(nblk > cur.pass);
-            cur.done = cur.mask == 0;
-        }
-        if (!cur.done) {
-            it.j[q] = __builtin_ctzll(cur.mask);
-            it.k[q] = cur.pass;
-            cur.mask &= cur.mask - 1;
-        } else {
-            it.j[q] = -1;
-            it.k[q] = 0;
-        }
-    }
+// Per-lane item descriptor.
+#define KEEP_IN (1u << 31)     // chunk belongs to a frame (else past the end)
+#define KEEP_WIN (1u << 30)    // chunk index < 8: window cell in bits 0-8
+#define KEEP_TAIL (1u << 29)   // frame's last chunk
+#define KEEP_RANK(k) (((k) >> 10) & 63u)
+
+__device__ __forceinline__ uint32_t bperm(uint32_t v, uint32_t r) {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(r << 2), (int)v);
 }
 
-// Issues the loads of a group: lane l reads chunk 64k + l of frame j.
-__device__ __forceinline__ void issue_items(const Items& it, uint4 (&v)[ZP_G], int lane,
-                                            uint32_t sb_lo, uint32_t sb_hi, uint32_t nch) {
+// Always issues exactly ZP_G loads (items past the end re-read the wave's
+// last chunk): a static load count keeps the compiler's s_waitcnt exact.
+__device__ __forceinline__ void issue_group(uint32_t g, uint32_t nitems, uint32_t pfx_lane,
+                                            Cursor& c, const Ranked& R, int lane,
+                                            uintptr_t fallback, uint4 (&v)[ZP_G],
+                                            uint32_t (&keep)[ZP_G]) {
+    uintptr_t a[ZP_G];
 #pragma unroll
     for (int q = 0; q < ZP_G; ++q) {
-        v[q] = make_uint4(0, 0, 0, 0);
-        if (it.j[q] >= 0) {
-            const int j = it.j[q];
-            const uint32_t c = it.k[q] * 64u + (uint32_t)lane;
-            const uintptr_t b = ((uintptr_t)rdl(sb_hi, j) << 32) | rdl(sb_lo, j);
+        const uint32_t i = g * ZP_G + q;
+        const uint32_t base = 64u * i, lim = base + 64u;
+        uint64_t F = 0;
+        while (c.rem && c.ns < lim) {                         // scalar: frames starting here
+            F |= 1ull << (c.ns - base);
+            c.rem &= c.rem - 1;
+            if (c.rem) c.ns = rdl(pfx_lane, (uint32_t)__builtin_ctzll(c.rem));
+        }
+        const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(F >> 32),
+                                   __builtin_amdgcn_mbcnt_lo((uint32_t)F, 0u));
+        const uint32_t r = c.rbase + below + (uint32_t)((F >> lane) & 1u);
+        c.rbase += (uint32_t)__builtin_popcountll(F);
+        const uint32_t vv = base + (uint32_t)lane;
+        const uint32_t olo = bperm(R.org_lo, r), ohi = bperm(R.org_hi, r);
+        const uint32_t lv = bperm(R.last, r), fp = bperm(R.pfx, r);
+        const uint32_t ci = vv - fp;                          // chunk index within the frame
+        uint32_t k = (r & 63u) << 10;
+        k |= ci < ZP_WIN_CH ? KEEP_WIN | (ci * 64u + ((r ^ ci) & 63u)) : 0u;
+        k |= vv == lv ? KEEP_TAIL : 0u;
+        keep[q] = (i < nitems && vv <= lv) ? k | KEEP_IN : 0u;
+        const uint32_t vc = vv < lv ? vv : lv;
+        a[q] = nitems ? (((uintptr_t)ohi << 32) | olo) + 16ull * vc : fallback;
+    }
 #ifndef ZP_ABL_STREAM_OFF
-            if (c < rdl(nch, j)) v[q] = ld_stream(b + 16ull * c);
+#pragma unroll
+    for (int q = 0; q < ZP_G; ++q) v[q] = ld_stream(a[q]);
 #endif
-        }
-    }
 }
 
-// Sums a landed group (full chunks only; lanes past the frame hold zeros)
-// and adds each item's total to its frame's lane.
-__device__ __forceinline__ void process_items(const Items& it, const uint4 (&v)[ZP_G], int lane,
-                                              uint32_t& vsum) {
+__device__ __forceinline__ void consume_group(uint32_t g, uint32_t nitems, int lane,
+                                              const uint4 (&v)[ZP_G], const uint32_t (&keep)[ZP_G],
+                                              uint4* win, uint4* tail, uint32_t* cend,
+                                              uint32_t& run) {
 #pragma unroll
     for (int q = 0; q < ZP_G; ++q) {
-        if (it.j[q] < 0) break;
+        const uint32_t i = g * ZP_G + q;
+        if (i >= nitems) break;                               // wave-uniform
+        const uint32_t k = keep[q];
+        if (k & KEEP_WIN) win[k & 0x1FFu] = v[q];
         uint32_t part = sad16(v[q].x, 0u);
         part = sad16(v[q].y, part);
         part = sad16(v[q].z, part);
         part = sad16(v[q].w, part);
-        const uint32_t tot = wave_total(part);
-        if (lane == it.j[q]) vsum += tot;
+        const uint32_t P = wave_scan(k & KEEP_IN ? part : 0u);
+        if (k & KEEP_TAIL) {
+            tail[KEEP_RANK(k)] = v[q];
+            cend[KEEP_RANK(k)] = run + P;
+        }
+        run += rdl(P, 63);
     }
+    // Retire the dummy loads of a short last group here: a load still in
+    // flight on some path makes the compiler wait vmcnt(0) at the next issue.
+#pragma unroll
+    for (int q = 0; q < ZP_G; ++q) asm volatile("" ::"v"(v[q].x), "v"(v[q].y), "v"(v[q].z), "v"(v[q].w));
 }
 
-#ifdef ZP_MINW
-__global__ void __launch_bounds__(64 * ZP_WAVES, ZP_MINW)
-#else
+// --------------------------------------------------------------------------
+// The batch kernel.
+// --------------------------------------------------------------------------
 __global__ void __launch_bounds__(64 * ZP_WAVES)
-#endif
 zp_parse_kernel(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs,
                 const uint32_t* __restrict__ lens, uint64_t n,
                 zp_record* __restrict__ records, zp_ext_offsets* __restrict__ inner_ext) {
-    // Per-wave LDS windows, dword-column-major: win[wave][dword][frame].
-    __shared__ uint32_t win[ZP_WAVES][ZP_WIN_DW][64];
+    // Per wave: header windows [8][64] + last chunks [64] (16-B cells), and
+    // the stream's running sum at each frame's last chunk.
+    __shared__ uint4 win_all[ZP_WAVES][(ZP_WIN_CH + 1) * 64];
+    __shared__ uint32_t cend_all[ZP_WAVES][64];
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
     const uint64_t f0 = ((uint64_t)blockIdx.x * ZP_WAVES + wid) * 64;
     if (f0 >= n) return;                       // whole wave past the batch (uniform)
+#ifdef ZP_STAMPS
+    const uint64_t wave_id = f0 / 64;
+#endif
+    STAMP(0);
     const uint64_t p = f0 + lane;
     const bool live = p < n;
     const uint32_t len = live ? lens[p] : 0;
     const uint8_t* g = arena + (live ? offs[p] : 0);
     const uintptr_t ga = (uintptr_t)g;
-    uint32_t* wcol = &win[wid][0][0];
-
-    // ---- A. window load: instruction k covers frames 8k..8k+7, 8 lanes each
-    // (128 contiguous bytes per frame), registers -> LDS columns.
-#ifndef ZP_ABL_WIN_OFF
-    {
-        const uint32_t alo = (uint32_t)ga, ahi = (uint32_t)(ga >> 32);
-#pragma unroll
-        for (int k = 0; k < ZP_WIN_CH; ++k) {
-            const int fr = k * 8 + (lane >> 3), ch = lane & 7;
-            const uint32_t fl = __shfl(len, fr, 64);
-            const uintptr_t fa = ((uintptr_t)(uint32_t)__shfl(ahi, fr, 64) << 32) |
-                                 (uint32_t)__shfl(alo, fr, 64);
-            const uintptr_t ca = (fa & ~(uintptr_t)15) + 16u * ch;
-            if (fl >= 64 && ca < fa + fl) {
-                uint4 v = *(const uint4*)ca;
-                const int col = fr ^ (ch << 2);
-                wcol[(ch * 4 + 0) * 64 + col] = v.x;
-                wcol[(ch * 4 + 1) * 64 + col] = v.y;
-                wcol[(ch * 4 + 2) * 64 + col] = v.z;
-                wcol[(ch * 4 + 3) * 64 + col] = v.w;
-            }
-        }
-    }
+    uint4* win = &win_all[wid][0];
+    uint4* tail = &win_all[wid][ZP_WIN_CH * 64];
+    uint32_t* cend = &cend_all[wid][0];
+#ifdef ZP_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
+    STAMP(1);
 
-    // ---- Stream range, fixed BEFORE the walk. Past the window the frame is
-    // 16-B aligned (the window ends at its 16-aligned base + 128), so the
-    // stream is the full chunks [wend, ea & ~15); the partial tail chunk is
-    // summed by the frame's own lane. Frames of 64 B..64 KiB only; the walk
-    // later corrects for an L4 start on either side of the window end.
+    // ---- stream setup: chunks [A & ~15, E) of frames of 64 B .. 64 KiB;
+    // longer frames stream their window only (exact checksum path).
     const uint32_t shift = (uint32_t)(ga & 15);
     const uint32_t wlen = len < ZP_WIN - shift ? len : ZP_WIN - shift;
     const bool giant = len > ZP_GIANT;
-    uint32_t nch = 0;
-    uintptr_t sbase = 0;
-    uint4 tail = make_uint4(0, 0, 0, 0);
-    uint32_t tail_n = 0;                     // valid bytes in the tail chunk
-    if (len >= 64 && !giant && wlen < len) {
-        const uintptr_t ea = ga + len;
-        sbase = ga + wlen;                   // 16-aligned
-        nch = (uint32_t)(((ea & ~(uintptr_t)15) - sbase) >> 4);
-        tail_n = (uint32_t)(ea & 15);
-        if (tail_n) tail = *(const uint4*)(ea & ~(uintptr_t)15);
+    const uint32_t span = giant ? (uint32_t)ZP_WIN : len + shift;
+    const uint32_t nch = len >= 64 ? (span + 15) >> 4 : 0u;
+    const uint64_t M = __ballot(nch > 0);
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(M >> 32),
+                              __builtin_amdgcn_mbcnt_lo((uint32_t)M, 0u));
+    const uint32_t incl = wave_scan(nch);
+    const uint32_t pfx = incl - nch;
+    const uint32_t T = rdl(incl, 63);
+    const uint32_t nitems = (T + 63) >> 6;
+    const uint32_t ngroups = (nitems + ZP_G - 1) / ZP_G;
+    Ranked R;
+    {   // compact the non-empty frames into rank order (tail cells as scratch)
+        const uintptr_t org = (ga & ~(uintptr_t)15) - 16ull * pfx;
+        if (nch) tail[rank] = make_uint4((uint32_t)org, (uint32_t)(org >> 32), incl - 1, pfx);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint4 t = tail[lane];            // lanes >= popcount(M): never selected
+        R.org_lo = t.x; R.org_hi = t.y; R.last = t.z; R.pfx = t.w;
     }
-    const uint32_t nblk = (nch + 63) >> 6;
-    const uint32_t sb_lo = (uint32_t)sbase, sb_hi = (uint32_t)(sbase >> 32);
     Cursor cur;
-    cur.mask = __ballot(nblk > 0);
-    cur.pass = 0;
-    cur.done = cur.mask == 0;
-    Items ia, ib;
-    uint4 va[ZP_G], vb[ZP_G];
-    fill_items(ia, cur, nblk);
-    issue_items(ia, va, lane, sb_lo, sb_hi, nch);      // in flight during the walk
+    cur.rem = M;
+    cur.ns = 0;                                // the first non-empty frame starts at 0
+    cur.rbase = ~0u;
+    const uintptr_t fallback = (uintptr_t)&zp_safe_chunk;   // only when T == 0
 
+    // ---- C. stream (+ windows and last chunks into LDS): one group of ZP_G
+    // items per iteration; no load is in flight across the loop back-edge.
+    uint4 va[ZP_G];
+    uint32_t ka[ZP_G];
+    uint32_t run = 0;
+    issue_group(0, nitems, pfx, cur, R, lane, fallback, va, ka);
+    // The compaction reads of `tail` must land before the stream overwrites it.
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    STAMP(2);
+    consume_group(0, nitems, lane, va, ka, win, tail, cend, run);
+    for (uint32_t gi = 1; gi < ngroups; ++gi) {
+        issue_group(gi, nitems, pfx, cur, R, lane, fallback, va, ka);
+        consume_group(gi, nitems, lane, va, ka, win, tail, cend, run);
+    }
     // LDS written by other lanes of this wave: order the wave's LDS ops.
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    STAMP(3);
 
-    // ---- B. walk (lane per frame)
+    // ---- B. walk (lane per frame; the window is indexed by rank)
     FrameView fv;
-    fv.col = wcol;
-    fv.lane = (uint32_t)lane;
+    fv.win = win;
     fv.g = g;
+    fv.lane = rank & 63u;
     fv.shift = shift;
     fv.len = len;
     fv.wlen = wlen;
@@ -572,48 +714,35 @@ zp_parse_kernel(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ 
     if (live) walk_frame(fv, w);
     else w.pending = 0;
 #endif
-    // L4 bytes inside the window and in the tail chunk, minus header bytes
-    // the stream covers.
-    uint32_t vsum = 0, vsub = 0;
-    if (w.pending && !giant) {
-        if (w.l4 < wlen) vsum = sumV(fv, w.l4, wlen);
-        else if (w.l4 > wlen) vsub = sumV(fv, wlen, w.l4);
-        if (tail_n) vsum = chunk_sum(tail, 0, (int)tail_n, vsum);
-    }
+    STAMP(4);
 
-    // ---- C. stream: two groups of ZP_G items in flight (ping-pong).
-    while (ia.j[0] >= 0) {
-        fill_items(ib, cur, nblk);
-        issue_items(ib, vb, lane, sb_lo, sb_hi, nch);
-        process_items(ia, va, lane, vsum);
-        if (ib.j[0] < 0) break;
-        fill_items(ia, cur, nblk);
-        issue_items(ia, va, lane, sb_lo, sb_hi, nch);
-        process_items(ib, vb, lane, vsum);
-    }
-
-    // ---- D. finalize + store
+    // ---- D. verdict + store. The frame's stream sum covers the whole chunks
+    // [A & ~15, E16): L4 sum = that - V[A & ~15, A + l4) - V[E, E16).
     if (!live) return;
-    zp_record r = w.rec;
+    zp_record rec = w.rec;
     if (w.pending) {
         bool ok;
         if (giant) {
             ok = csum_ok_exact(g, w.l4, len, w.acc);
         } else {
-            bool odd = (ga + w.l4) & 1;
-            ok = csum_ok(w.acc, vsum - vsub, odd);
+            const bool odd = (ga + w.l4) & 1;
+            const uint32_t fsum = cend[rank] - (rank ? cend[rank - 1] : 0u);
+            const uint32_t he = (len + shift) & 15u;      // bytes of the last chunk in use
+            const uint32_t ex = he ? range_sum(tail[rank], he, 16u) : 0u;
+            ok = csum_ok(w.acc, fsum - sumV(fv, 0, w.l4) - sum_head(fv) - ex, odd);
         }
         if (!ok) {
-            r = zp_record{};
-            r.err = (uint8_t)(w.v6 ? ZP_ERR_IPV6_L4_CHECKSUM : ZP_ERR_IPV4_L4_CHECKSUM);
+            rec = zp_record{};
+            rec.err = (uint8_t)(w.v6 ? ZP_ERR_IPV6_L4_CHECKSUM : ZP_ERR_IPV4_L4_CHECKSUM);
         }
     }
+    STAMP(5);
     uint4 q2[2];
-    memcpy(q2, &r, sizeof r);
+    memcpy(q2, &rec, sizeof rec);
     uint4* dst = (uint4*)(records + p);
     dst[0] = q2[0];
     dst[1] = q2[1];
-    if (inner_ext && (r.flags & ZP_F_INNER_EXT)) inner_ext[p] = w.inner;
+    if (inner_ext && (rec.flags & ZP_F_INNER_EXT)) inner_ext[p] = w.inner;
 }
 
 // --------------------------------------------------------------------------
@@ -628,14 +757,14 @@ extern "C" int zp_parse_batch_device(const uint8_t* arena, const uint64_t* offs,
         snprintf(g_last_error, sizeof g_last_error, "zp_parse_batch_device: null pointer");
         return -1;
     }
-    uint64_t blocks = (n + 64 * ZP_WAVES - 1) / (64 * ZP_WAVES);
+    const uint64_t blocks = (n + 64 * ZP_WAVES - 1) / (64 * ZP_WAVES);
     if (blocks > 0x7FFFFFFFull) {
         snprintf(g_last_error, sizeof g_last_error, "zp_parse_batch_device: batch too large");
         return -1;
     }
     hipLaunchKernelGGL(zp_parse_kernel, dim3((unsigned)blocks), dim3(64 * ZP_WAVES), 0,
                        (hipStream_t)stream, arena, offs, lens, n, records, inner_ext);
-    hipError_t e = hipGetLastError();
+    const hipError_t e = hipGetLastError();
     if (e != hipSuccess) { set_err("zp_parse_kernel launch", e); return -2; }
     return 0;
 }
