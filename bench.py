@@ -49,6 +49,18 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def pmc_traffic(config, frames, nbytes):
+    """HBM read bytes per launch from the committed PMC pass of this workload
+    (tools/pmc_traffic.sh -> profiles/*_traffic_<config>.json), or None."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_traffic_{config}.json")),
+                       reverse=True):
+        t = json.load(open(path))
+        if t.get("frames_per_launch") == frames and t.get("algorithmic_bytes_per_launch") == nbytes:
+            return int(t["read_bytes_per_launch"]), os.path.relpath(path, ROOT)
+    return None, None
+
+
 def cpu_baseline(zp, arena, offs, lens, sample_pkts, min_seconds):
     """Times the oracle (C port, all threads of this process' CPU share) on the
     first `sample_pkts` frames, copied to host memory."""
@@ -69,10 +81,23 @@ def cpu_baseline(zp, arena, offs, lens, sample_pkts, min_seconds):
             break
     assert (rec["err"] == 0).all()
     sec = dt / reps
+    # the same port on one core, on the first eighth of the sample
+    m1 = max(1, m // 8)
+    reps1, t1 = 0, time.perf_counter()
+    while True:
+        orc.parse_batch(a, o[:m1], ln[:m1], 1)
+        reps1 += 1
+        dt1 = time.perf_counter() - t1
+        if dt1 >= min_seconds / 2:
+            break
+    sec1 = dt1 / reps1
     return {"value": round(m / sec / 1e6, 3), "unit": "Mpkt/s", "cores": threads,
             "kind": "port", "gb_per_s": round(float(ln.sum()) / sec / 1e9, 3),
+            "value_1core": round(m1 / sec1 / 1e6, 3),
+            "gb_per_s_1core": round(float(ln[:m1].sum()) / sec1 / 1e9, 3),
             "sample": f"first {m} frames of the timed batch ({float(ln.sum())/1e9:.2f} GB), "
-                      f"{reps} passes, oracle/zp_oracle.c with {threads} threads"}
+                      f"{reps} passes, oracle/zp_oracle.c with {threads} threads; 1-core: "
+                      f"first {m1} frames, {reps1} passes"}
 
 
 def pcie_inclusive(zp, arena, offs, lens, sample_pkts):
@@ -159,6 +184,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
 
+    traffic, traffic_src = pmc_traffic(args.config, n, total_bytes)
     ms_step = elapsed / args.steps * 1e3
     pkts = n * world * args.steps
     mpkts = pkts / elapsed / 1e6
@@ -178,7 +204,8 @@ def main():
                    "parallelism": f"dp{world} (independent shards, no collective)"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": None, "kernel": "zp_parse_kernel",
+                     "traffic": traffic, "traffic_source": traffic_src,
+                     "kernel": "zp_parse_kernel",
                      "kernel_ms_mean": round(kmean, 4), "kernel_ms_min": round(min(kms), 4),
                      "algorithmic_bytes_per_launch": total_bytes},
     }

@@ -1,0 +1,429 @@
+// zero_packet.hpp — C++17 facade over the C ABI (include/zero_packet.h) that
+// mirrors the reference's public parse API:
+//
+//   PacketParser::parse(&[u8]) -> Result<PacketParser, &'static str>
+//                                       (/root/reference/src/packet/parser.rs:53)
+//   struct PacketParser { ethernet, arp, ipv4, ipv6, ip_in_ip, tcp, udp,
+//                         icmpv4, icmpv6 }   (parser.rs:22-32)
+//   the *Reader views and their getters      (src/datalink, src/network,
+//                                             src/transport)
+//
+// Every reader is a view `frame[start..]` that runs to the end of the frame,
+// like the reference's `&'a [u8]` sub-slices (zero copy; the frame must
+// outlive the views). A PacketParser is rebuilt from a zp_record without
+// re-parsing (PacketParser::from_record). Errors are zp::Error carrying the
+// zp_err code and the exact reference string. Header-only; parse() and the
+// batch calls need libzp_hip.so (the GPU path), from_record() does not.
+#ifndef ZERO_PACKET_HPP
+#define ZERO_PACKET_HPP
+
+#include <array>
+#include <cstddef>
+#include <cstdint>
+#include <optional>
+#include <stdexcept>
+#include <string>
+#include <utility>
+
+#include "zero_packet.h"
+#include "zero_packet_errstr.h"
+
+namespace zp {
+
+// The `&'static str` of the reference's Err, with its zp_err code.
+class Error : public std::runtime_error {
+public:
+    Error(int code, const char* msg) : std::runtime_error(msg ? msg : "zero-packet error"),
+                                       code_(code) {}
+    int code() const { return code_; }
+private:
+    int code_;
+};
+
+// A borrowed byte slice (&'a [u8]).
+struct Bytes {
+    const uint8_t* ptr = nullptr;
+    size_t len = 0;
+    size_t size() const { return len; }
+    const uint8_t& operator[](size_t i) const { return ptr[i]; }
+    Bytes sub(size_t from) const { return from <= len ? Bytes{ptr + from, len - from} : Bytes{ptr + len, 0}; }
+    Bytes sub(size_t from, size_t to) const { return Bytes{ptr + from, to - from}; }
+};
+
+namespace detail {
+inline uint16_t be16(Bytes b, size_t i) { return (uint16_t)((b[i] << 8) | b[i + 1]); }
+inline uint32_t be32(Bytes b, size_t i) {
+    return ((uint32_t)b[i] << 24) | ((uint32_t)b[i + 1] << 16) | ((uint32_t)b[i + 2] << 8) | b[i + 3];
+}
+template <size_t N> std::array<uint8_t, N> arr(Bytes b, size_t i) {
+    std::array<uint8_t, N> a{};
+    for (size_t k = 0; k < N; ++k) a[k] = b[i + k];
+    return a;
+}
+[[noreturn]] inline void fail(int code) { throw Error(code, zp_err_string(code)); }
+}  // namespace detail
+
+// ethernet.rs:131-263
+class EthernetReader {
+public:
+    Bytes bytes;
+    EthernetReader(Bytes b, size_t header_len) : bytes(b), hl_(header_len) {}
+    std::array<uint8_t, 6> dest_mac() const { return detail::arr<6>(bytes, 0); }
+    std::array<uint8_t, 6> src_mac() const { return detail::arr<6>(bytes, 6); }
+    uint16_t ethertype() const { return detail::be16(bytes, hl_ - 2); }
+    bool is_vlan_tagged() const { return detail::be16(bytes, 12) == 0x8100; }
+    bool is_vlan_double_tagged() const { return detail::be16(bytes, 12) == 0x88A8; }
+    // (tpid, tci) of a single 802.1Q tag (ethernet.rs:218-227)
+    std::optional<std::pair<uint16_t, uint16_t>> vlan_tag() const {
+        if (!is_vlan_tagged()) return std::nullopt;
+        return std::make_pair(detail::be16(bytes, 12), detail::be16(bytes, 14));
+    }
+    // ((tpid, tci), (tpid, tci)) of a Q-in-Q pair (ethernet.rs:233-244)
+    std::optional<std::pair<std::pair<uint16_t, uint16_t>, std::pair<uint16_t, uint16_t>>>
+    double_vlan_tag() const {
+        if (!is_vlan_double_tagged()) return std::nullopt;
+        return std::make_pair(std::make_pair(detail::be16(bytes, 12), detail::be16(bytes, 14)),
+                              std::make_pair(detail::be16(bytes, 16), detail::be16(bytes, 18)));
+    }
+    size_t header_len() const { return hl_; }
+    Bytes header() const { return bytes.sub(0, hl_); }
+    Bytes payload() const { return bytes.sub(hl_); }
+private:
+    size_t hl_;
+};
+
+// arp.rs:121-227
+class ArpReader {
+public:
+    Bytes bytes;
+    explicit ArpReader(Bytes b) : bytes(b) {}
+    uint16_t htype() const { return detail::be16(bytes, 0); }
+    uint16_t ptype() const { return detail::be16(bytes, 2); }
+    uint8_t hlen() const { return bytes[4]; }
+    uint8_t plen() const { return bytes[5]; }
+    uint16_t oper() const { return detail::be16(bytes, 6); }
+    std::array<uint8_t, 6> sha() const { return detail::arr<6>(bytes, 8); }
+    std::array<uint8_t, 4> spa() const { return detail::arr<4>(bytes, 14); }
+    std::array<uint8_t, 6> tha() const { return detail::arr<6>(bytes, 18); }
+    std::array<uint8_t, 4> tpa() const { return detail::arr<4>(bytes, 24); }
+    size_t header_len() const { return 28; }
+    Bytes header() const { return bytes.sub(0, 28); }
+    Bytes payload() const { return bytes.sub(28); }
+};
+
+// ipv4.rs:129-265
+class IPv4Reader {
+public:
+    Bytes bytes;
+    explicit IPv4Reader(Bytes b) : bytes(b) {}
+    uint8_t version() const { return bytes[0] >> 4; }
+    uint8_t ihl() const { return bytes[0] & 0x0F; }
+    uint8_t dscp() const { return bytes[1] >> 2; }
+    uint8_t ecn() const { return bytes[1] & 0x03; }
+    uint16_t total_length() const { return detail::be16(bytes, 2); }
+    uint16_t id() const { return detail::be16(bytes, 4); }
+    uint8_t flags() const { return bytes[6] >> 5; }
+    uint16_t fragment_offset() const { return (uint16_t)(((bytes[6] & 0x1F) << 8) | bytes[7]); }
+    uint8_t ttl() const { return bytes[8]; }
+    uint8_t protocol() const { return bytes[9]; }
+    uint16_t checksum() const { return detail::be16(bytes, 10); }
+    std::array<uint8_t, 4> src_ip() const { return detail::arr<4>(bytes, 12); }
+    std::array<uint8_t, 4> dest_ip() const { return detail::arr<4>(bytes, 16); }
+    size_t header_len() const { return (size_t)ihl() * 4; }
+    Bytes header() const { check(); return bytes.sub(0, header_len()); }
+    Bytes payload() const { check(); return bytes.sub(header_len()); }
+private:
+    void check() const {   // ipv4.rs:238-241,252-255
+        if (header_len() > bytes.size())
+            detail::fail(ZP_ERR_IPV4_HDR_EXCEEDS);
+    }
+};
+
+// extensions/options.rs:76-154 (Hop-by-Hop, Destination Options)
+class OptionsHeaderReader {
+public:
+    Bytes bytes;
+    explicit OptionsHeaderReader(Bytes b) : bytes(b) {}
+    uint8_t next_header() const { return bytes[0]; }
+    uint8_t header_ext_len() const { return bytes[1]; }
+    size_t header_len() const { return ((size_t)bytes[1] + 1) * 8; }
+    Bytes header() const { check(); return bytes.sub(0, header_len()); }
+    Bytes payload() const { check(); return bytes.sub(header_len()); }
+private:
+    void check() const {
+        if (header_len() > bytes.size())
+            detail::fail(ZP_ERR_EXT_OPTIONS_EXCEEDS);
+    }
+};
+
+// extensions/routing.rs:99-195
+class RoutingHeaderReader {
+public:
+    Bytes bytes;
+    explicit RoutingHeaderReader(Bytes b) : bytes(b) {}
+    uint8_t next_header() const { return bytes[0]; }
+    uint8_t header_ext_len() const { return bytes[1]; }
+    uint8_t routing_type() const { return bytes[2]; }
+    uint8_t segments_left() const { return bytes[3]; }
+    size_t header_len() const { return ((size_t)bytes[1] + 1) * 8; }
+    Bytes header() const { check(); return bytes.sub(0, header_len()); }
+    Bytes payload() const { check(); return bytes.sub(header_len()); }
+private:
+    void check() const {
+        if (header_len() > bytes.size())
+            detail::fail(ZP_ERR_EXT_ROUTING_EXCEEDS);
+    }
+};
+
+// extensions/fragment.rs:90-173
+class FragmentHeaderReader {
+public:
+    Bytes bytes;
+    explicit FragmentHeaderReader(Bytes b) : bytes(b) {}
+    uint8_t next_header() const { return bytes[0]; }
+    uint8_t reserved() const { return bytes[1]; }
+    uint16_t fragment_offset() const { return (uint16_t)((bytes[2] << 5) | (bytes[3] & 0x1F)); }
+    uint8_t res() const { return (bytes[3] >> 5) & 0x3; }
+    bool m_flag() const { return (bytes[3] & 0x80) != 0; }
+    uint32_t identification() const { return detail::be32(bytes, 4); }
+    size_t header_len() const { return 8; }
+    Bytes header() const { return bytes.sub(0, 8); }
+    Bytes payload() const { return bytes.sub(8); }
+};
+
+// extensions/authentication.rs:97-200
+class AuthenticationHeaderReader {
+public:
+    Bytes bytes;
+    explicit AuthenticationHeaderReader(Bytes b) : bytes(b) {}
+    uint8_t next_header() const { return bytes[0]; }
+    uint8_t payload_len() const { return bytes[1]; }
+    uint16_t reserved() const { return detail::be16(bytes, 2); }
+    uint32_t spi() const { return detail::be32(bytes, 4); }
+    uint32_t sequence_number() const { return detail::be32(bytes, 8); }
+    size_t header_len() const { return ((size_t)bytes[1] + 2) * 4; }
+    Bytes header() const { check(); return bytes.sub(0, header_len()); }
+    Bytes payload() const { check(); return bytes.sub(header_len()); }
+private:
+    void check() const {
+        if (header_len() > bytes.size())
+            detail::fail(ZP_ERR_EXT_AUTH_EXCEEDS);
+    }
+};
+
+// extensions/headers.rs:19-28
+struct ExtensionHeaders {
+    std::optional<OptionsHeaderReader> hop_by_hop;
+    std::optional<RoutingHeaderReader> routing;
+    std::optional<FragmentHeaderReader> fragment;
+    std::optional<AuthenticationHeaderReader> auth_header;
+    std::optional<OptionsHeaderReader> destination_1st;
+    std::optional<OptionsHeaderReader> destination_2nd;
+    size_t total_headers_len = 0;
+    uint8_t final_next_header = 0;
+};
+
+// ipv6.rs:135-286
+class IPv6Reader {
+public:
+    Bytes bytes;
+    std::optional<ExtensionHeaders> extension_headers;
+    size_t extension_headers_len = 0;
+    explicit IPv6Reader(Bytes b) : bytes(b) {}
+    uint8_t version() const { return bytes[0] >> 4; }
+    uint8_t traffic_class() const { return (uint8_t)(((bytes[0] & 0x0F) << 4) | (bytes[1] >> 4)); }
+    uint32_t flow_label() const {
+        return ((uint32_t)(bytes[1] & 0x0F) << 16) | ((uint32_t)bytes[2] << 8) | bytes[3];
+    }
+    uint16_t payload_length() const { return detail::be16(bytes, 4); }
+    uint8_t next_header() const { return bytes[6]; }
+    uint8_t final_next_header() const {   // ipv6.rs:219-227
+        return extension_headers ? extension_headers->final_next_header : next_header();
+    }
+    uint8_t hop_limit() const { return bytes[7]; }
+    std::array<uint8_t, 16> src_addr() const { return detail::arr<16>(bytes, 8); }
+    std::array<uint8_t, 16> dest_addr() const { return detail::arr<16>(bytes, 24); }
+    size_t header_len() const { return 40; }
+    Bytes header() const { return bytes.sub(0, 40); }
+    Bytes payload() const { return bytes.sub(40); }
+    Bytes upper_layer_payload() const { return bytes.sub(40 + extension_headers_len); }
+};
+
+// tcp.rs:132-244
+class TcpReader {
+public:
+    Bytes bytes;
+    explicit TcpReader(Bytes b) : bytes(b) {}
+    uint16_t src_port() const { return detail::be16(bytes, 0); }
+    uint16_t dest_port() const { return detail::be16(bytes, 2); }
+    uint32_t sequence_number() const { return detail::be32(bytes, 4); }
+    uint32_t ack_number() const { return detail::be32(bytes, 8); }
+    uint8_t data_offset() const { return bytes[12] >> 4; }
+    uint8_t reserved() const { return bytes[12] & 0x0F; }
+    uint8_t flags() const { return bytes[13]; }
+    uint16_t window_size() const { return detail::be16(bytes, 14); }
+    uint16_t checksum() const { return detail::be16(bytes, 16); }
+    uint16_t urgent_pointer() const { return detail::be16(bytes, 18); }
+    size_t header_len() const { return (size_t)data_offset() * 4; }
+};
+
+// udp.rs:94-154
+class UdpReader {
+public:
+    Bytes bytes;
+    explicit UdpReader(Bytes b) : bytes(b) {}
+    uint16_t src_port() const { return detail::be16(bytes, 0); }
+    uint16_t dest_port() const { return detail::be16(bytes, 2); }
+    uint16_t length() const { return detail::be16(bytes, 4); }
+    uint16_t checksum() const { return detail::be16(bytes, 6); }
+    size_t header_len() const { return 8; }
+    Bytes header() const { return bytes.sub(0, 8); }
+    Bytes payload() const { return bytes.sub(8); }
+};
+
+// icmpv4.rs:83-135 / icmpv6.rs:80-132
+class IcmpReader {
+public:
+    Bytes bytes;
+    explicit IcmpReader(Bytes b) : bytes(b) {}
+    uint8_t icmp_type() const { return bytes[0]; }
+    uint8_t icmp_code() const { return bytes[1]; }
+    uint16_t checksum() const { return detail::be16(bytes, 2); }
+    size_t header_len() const { return 8; }
+    Bytes header() const { return bytes.sub(0, 8); }
+    Bytes payload() const { return bytes.sub(8); }
+};
+class Icmpv4Reader : public IcmpReader { using IcmpReader::IcmpReader; };
+class Icmpv6Reader : public IcmpReader { using IcmpReader::IcmpReader; };
+
+// misc.rs:6-9: IpInIp::Ipv4(IPv4Reader) | IpInIp::Ipv6(IPv6Reader)
+struct IpInIp {
+    enum class Kind { Ipv4, Ipv6 } kind;
+    std::optional<IPv4Reader> ipv4;
+    std::optional<IPv6Reader> ipv6;
+};
+
+// parser.rs:22-32
+struct PacketParser {
+    std::optional<EthernetReader> ethernet;
+    std::optional<ArpReader> arp;
+    std::optional<IPv4Reader> ipv4;
+    std::optional<IPv6Reader> ipv6;
+    std::optional<IpInIp> ip_in_ip;
+    std::optional<TcpReader> tcp;
+    std::optional<UdpReader> udp;
+    std::optional<Icmpv4Reader> icmpv4;
+    std::optional<Icmpv6Reader> icmpv6;
+
+    // Rebuilds the parse result of `frame` from its record (no re-parse).
+    // Throws zp::Error when the record holds an error (the reference's Err).
+    static PacketParser from_record(Bytes frame, const zp_record& r,
+                                    const zp_ext_offsets* inner = nullptr) {
+        if (r.err) detail::fail(r.err);
+        PacketParser p;
+        const size_t hl = r.eth_len;
+        if (r.flags & ZP_F_ETHERNET) p.ethernet.emplace(frame, hl);
+        if (r.flags & ZP_F_ARP) p.arp.emplace(frame.sub(hl));
+        if (r.flags & ZP_F_IPV4) p.ipv4.emplace(frame.sub(hl));
+        if (r.flags & ZP_F_IPV6) {
+            IPv6Reader v6(frame.sub(hl));
+            if (r.flags & ZP_F_EXT) {
+                v6.extension_headers = ext(frame, hl + 40, r.flags, 12, r.ext_off, r.ext_len,
+                                           r.final_nh);
+                v6.extension_headers_len = r.ext_len;
+            }
+            p.ipv6 = v6;
+        }
+        if (r.flags & ZP_F_IP_IN_IP) {
+            IpInIp ii;
+            if (r.flags & ZP_F_IP_IN_IP_V6) {
+                ii.kind = IpInIp::Kind::Ipv6;
+                IPv6Reader v6(frame.sub(r.inner_off));
+                if (r.flags & ZP_F_INNER_EXT) {
+                    static const uint16_t zero[ZP_EXT_SLOTS] = {0, 0, 0, 0, 0, 0};
+                    v6.extension_headers = ext(frame, r.inner_off + 40, r.flags, 18,
+                                               inner ? inner->off : zero, r.inner_ext_len,
+                                               r.inner_final_nh);
+                    v6.extension_headers_len = r.inner_ext_len;
+                }
+                ii.ipv6 = v6;
+            } else {
+                ii.kind = IpInIp::Kind::Ipv4;
+                ii.ipv4.emplace(frame.sub(r.inner_off));
+            }
+            p.ip_in_ip = ii;
+        }
+        const Bytes l4 = frame.sub(r.l4_off);
+        if (r.flags & ZP_F_TCP) p.tcp.emplace(l4);
+        if (r.flags & ZP_F_UDP) p.udp.emplace(l4);
+        if (r.flags & ZP_F_ICMPV4) p.icmpv4.emplace(l4);
+        if (r.flags & ZP_F_ICMPV6) p.icmpv6.emplace(l4);
+        return p;
+    }
+
+    // PacketParser::parse (parser.rs:53) for one frame, through the GPU path
+    // (zp_parse_one on `ctx`). Throws zp::Error on a parse error and
+    // std::runtime_error on a HIP failure.
+    static PacketParser parse(zp_ctx* ctx, Bytes frame, zp_ext_offsets* inner_out = nullptr) {
+        zp_record r{};
+        zp_ext_offsets e{};
+        const int rc = zp_parse_one(ctx, frame.ptr, frame.len, &r, &e);
+        if (rc < 0) throw std::runtime_error(std::string("zp_parse_one: ") + zp_last_error());
+        if (inner_out) *inner_out = e;
+        return from_record(frame, r, &e);
+    }
+
+private:
+    static ExtensionHeaders ext(Bytes frame, size_t payload_off, uint32_t flags, int shift,
+                                const uint16_t* off, size_t total, uint8_t final_nh) {
+        ExtensionHeaders eh;
+        auto at = [&](int k) { return frame.sub(payload_off + off[k]); };
+        if (flags & (1u << (shift + ZP_EXT_HBH))) eh.hop_by_hop.emplace(at(ZP_EXT_HBH));
+        if (flags & (1u << (shift + ZP_EXT_RT))) eh.routing.emplace(at(ZP_EXT_RT));
+        if (flags & (1u << (shift + ZP_EXT_FRAG))) eh.fragment.emplace(at(ZP_EXT_FRAG));
+        if (flags & (1u << (shift + ZP_EXT_AH))) eh.auth_header.emplace(at(ZP_EXT_AH));
+        if (flags & (1u << (shift + ZP_EXT_DST1))) eh.destination_1st.emplace(at(ZP_EXT_DST1));
+        if (flags & (1u << (shift + ZP_EXT_DST2))) eh.destination_2nd.emplace(at(ZP_EXT_DST2));
+        eh.total_headers_len = total;
+        eh.final_next_header = final_nh;
+        return eh;
+    }
+};
+
+// RAII owner of a zp_ctx (host-memory batches, single frames).
+class Context {
+public:
+    explicit Context(int device = 0, uint64_t chunk_bytes = 0)
+        : ctx_(zp_ctx_create(device, chunk_bytes)) {
+        if (!ctx_) throw std::runtime_error(std::string("zp_ctx_create: ") + zp_last_error());
+    }
+    ~Context() { zp_ctx_destroy(ctx_); }
+    Context(const Context&) = delete;
+    Context& operator=(const Context&) = delete;
+    zp_ctx* get() const { return ctx_; }
+
+    // n frames of a host buffer -> host records (H2D, parse, D2H).
+    void parse_batch(const uint8_t* arena, uint64_t arena_bytes, const uint64_t* offs,
+                     const uint32_t* lens, uint64_t n, zp_record* records,
+                     zp_ext_offsets* inner_ext = nullptr) {
+        if (zp_parse_batch_host(ctx_, arena, arena_bytes, offs, lens, n, records, inner_ext) < 0)
+            throw std::runtime_error(std::string("zp_parse_batch_host: ") + zp_last_error());
+    }
+    PacketParser parse(Bytes frame, zp_ext_offsets* inner_out = nullptr) {
+        return PacketParser::parse(ctx_, frame, inner_out);
+    }
+private:
+    zp_ctx* ctx_;
+};
+
+// Device-resident batch (the hot path): enqueue on a hipStream_t (void*).
+inline void parse_batch_device(const uint8_t* arena, const uint64_t* offs, const uint32_t* lens,
+                               uint64_t n, zp_record* records, zp_ext_offsets* inner_ext,
+                               void* stream) {
+    if (zp_parse_batch_device(arena, offs, lens, n, records, inner_ext, stream) < 0)
+        throw std::runtime_error(std::string("zp_parse_batch_device: ") + zp_last_error());
+}
+
+}  // namespace zp
+
+#endif  // ZERO_PACKET_HPP

@@ -1,12 +1,12 @@
 /*
- * zp_errstr.h — exact reference error strings for each zp_err code.
+ * zero_packet_errstr.h — exact reference error strings for each zp_err code.
  * Each string is the `&'static str` the reference returns (file:line given
  * in include/zero_packet.h next to the code).
  */
-#ifndef ZP_ERRSTR_H
-#define ZP_ERRSTR_H
+#ifndef ZERO_PACKET_ERRSTR_H
+#define ZERO_PACKET_ERRSTR_H
 
-#include "../../include/zero_packet.h"
+#include "zero_packet.h"
 
 static const char* const zp_err_strings[ZP_ERR_COUNT] = {
     "",
@@ -52,4 +52,4 @@ static inline const char* zp_err_string(int code) {
     return zp_err_strings[code];
 }
 
-#endif /* ZP_ERRSTR_H */
+#endif /* ZERO_PACKET_ERRSTR_H */

@@ -43,7 +43,7 @@
 #include <stdlib.h>
 
 #include "../../include/zero_packet.h"
-#include "zp_errstr.h"
+#include "../../include/zero_packet_errstr.h"
 
 #define ZP_WIN 128           // window bytes per frame
 #define ZP_WIN_CH (ZP_WIN / 16)
