@@ -523,10 +523,10 @@ __device__ __forceinline__ uint32_t range_sum(uint4 v, uint32_t lo, uint32_t hi)
 // The first 8 chunks of each frame (the header window) and its last chunk
 // are also written to LDS for the walk and the verdict.
 // --------------------------------------------------------------------------
-struct Cursor {          // wave-uniform (SGPRs)
-    uint64_t rem;        // ranks whose first chunk is not yet passed (lane mask)
-    uint32_t ns;         // first virtual chunk of the next such frame
+struct Cursor {          // wave-uniform
     uint32_t rbase;      // rank of the frame holding the chunk before the item
+    uint32_t nz;         // number of ranks (frames that own chunks)
+    uint64_t* starts;    // LDS: starts[i & 63] = bit b set <=> a frame starts at 64i + b
 };
 
 struct Ranked {          // lane r = frame of rank r
@@ -547,24 +547,46 @@ __device__ __forceinline__ uint32_t bperm(uint32_t v, uint32_t r) {
 
 // Always issues exactly ZP_G loads (items past the end re-read the wave's
 // last chunk): a static load count keeps the compiler's s_waitcnt exact.
-__device__ __forceinline__ void issue_group(uint32_t g, uint32_t nitems, uint32_t pfx_lane,
-                                            Cursor& c, const Ranked& R, int lane,
-                                            uintptr_t fallback, uint4 (&v)[ZP_G],
-                                            uint32_t (&keep)[ZP_G]) {
+// Rebuilds the start masks of items [w0, w0 + 64): one LDS atomic OR per
+// frame starting there. Straight-line code (no loop): a loop here would make
+// LLVM's wait-count insertion drain the group in flight (vmcnt(0)).
+__device__ __forceinline__ void build_starts(uint32_t w0, const Cursor& c, const Ranked& R,
+                                             int lane) {
+    c.starts[lane] = 0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint32_t it = R.pfx >> 6;
+    if ((uint32_t)lane < c.nz && it >= w0 && it < w0 + 64u)
+        __hip_atomic_fetch_or(&c.starts[it - w0], 1ull << (R.pfx & 63u), __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_WAVEFRONT);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Always issues exactly ZP_G loads (items past the end re-read the wave's
+// last chunk): a static load count keeps the compiler's s_waitcnt exact.
+__device__ __forceinline__ void issue_group(uint32_t g, uint32_t nitems, Cursor& c,
+                                            const Ranked& R, int lane, uintptr_t fallback,
+                                            uint4 (&v)[ZP_G], uint32_t (&keep)[ZP_G]) {
     uintptr_t a[ZP_G];
 #pragma unroll
     for (int q = 0; q < ZP_G; ++q) {
         const uint32_t i = g * ZP_G + q;
-        const uint32_t base = 64u * i, lim = base + 64u;
+        const uint32_t base = 64u * i;
+        if ((i & 63u) == 0 && i < nitems) build_starts(i, c, R, lane);   // wave-uniform
         uint64_t F = 0;
-        while (c.rem && c.ns < lim) {                         // scalar: frames starting here
-            F |= 1ull << (c.ns - base);
-            c.rem &= c.rem - 1;
-            if (c.rem) c.ns = rdl(pfx_lane, (uint32_t)__builtin_ctzll(c.rem));
+        if (i < nitems) {
+            const uint64_t f = c.starts[i & 63u];
+            // (readfirstlane returns int: cast before widening, no sign extension)
+            F = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(f >> 32)) << 32) |
+                (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)f);
         }
         const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(F >> 32),
                                    __builtin_amdgcn_mbcnt_lo((uint32_t)F, 0u));
-        const uint32_t r = c.rbase + below + (uint32_t)((F >> lane) & 1u);
+        uint32_t r = c.rbase + below + (uint32_t)((F >> lane) & 1u);
+        r = r < c.nz ? r : c.nz - 1u;       // past the last frame (and never a stray lane)
         c.rbase += (uint32_t)__builtin_popcountll(F);
         const uint32_t vv = base + (uint32_t)lane;
         const uint32_t olo = bperm(R.org_lo, r), ohi = bperm(R.org_hi, r);
@@ -581,6 +603,16 @@ __device__ __forceinline__ void issue_group(uint32_t g, uint32_t nitems, uint32_
 #pragma unroll
     for (int q = 0; q < ZP_G; ++q) v[q] = ld_stream(a[q]);
 #endif
+    // Compiler barrier: keeps LLVM from sinking the loads below the consume
+    // of the previous group (which would serialise the double buffer).
+    asm volatile("" ::: "memory");
+}
+
+// An empty asm that reads every register of the group: forces the wait for
+// all of its loads at this point.
+__device__ __forceinline__ void retire_group(const uint4 (&v)[ZP_G]) {
+#pragma unroll
+    for (int q = 0; q < ZP_G; ++q) asm volatile("" ::"v"(v[q].x), "v"(v[q].y), "v"(v[q].z), "v"(v[q].w));
 }
 
 __device__ __forceinline__ void consume_group(uint32_t g, uint32_t nitems, int lane,
@@ -606,8 +638,7 @@ __device__ __forceinline__ void consume_group(uint32_t g, uint32_t nitems, int l
     }
     // Retire the dummy loads of a short last group here: a load still in
     // flight on some path makes the compiler wait vmcnt(0) at the next issue.
-#pragma unroll
-    for (int q = 0; q < ZP_G; ++q) asm volatile("" ::"v"(v[q].x), "v"(v[q].y), "v"(v[q].z), "v"(v[q].w));
+    retire_group(v);
 }
 
 // --------------------------------------------------------------------------
@@ -621,6 +652,7 @@ zp_parse_kernel(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ 
     // the stream's running sum at each frame's last chunk.
     __shared__ uint4 win_all[ZP_WAVES][(ZP_WIN_CH + 1) * 64];
     __shared__ uint32_t cend_all[ZP_WAVES][64];
+    __shared__ uint64_t starts_all[ZP_WAVES][64];
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
     const uint64_t f0 = ((uint64_t)blockIdx.x * ZP_WAVES + wid) * 64;
@@ -668,9 +700,9 @@ zp_parse_kernel(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ 
         R.org_lo = t.x; R.org_hi = t.y; R.last = t.z; R.pfx = t.w;
     }
     Cursor cur;
-    cur.rem = M;
-    cur.ns = 0;                                // the first non-empty frame starts at 0
     cur.rbase = ~0u;
+    cur.nz = (uint32_t)__builtin_popcountll(M);
+    cur.starts = &starts_all[wid][0];
     const uintptr_t fallback = (uintptr_t)&zp_safe_chunk;   // only when T == 0
 
     // ---- C. stream (+ windows and last chunks into LDS): one group of ZP_G
@@ -678,17 +710,47 @@ zp_parse_kernel(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ 
     uint4 va[ZP_G];
     uint32_t ka[ZP_G];
     uint32_t run = 0;
-    issue_group(0, nitems, pfx, cur, R, lane, fallback, va, ka);
+    issue_group(0, nitems, cur, R, lane, fallback, va, ka);
     // The compaction reads of `tail` must land before the stream overwrites it.
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     STAMP(2);
+#if defined(ZP_DB2)
+    // Double-buffered, both groups issued ahead: each iteration consumes a
+    // group and immediately re-issues into the registers it just drained.
+    uint4 vb[ZP_G];
+    uint32_t kb[ZP_G];
+    issue_group(1, nitems, cur, R, lane, fallback, vb, kb);
+    for (uint32_t gi = 0;; gi += 2) {
+        consume_group(gi, nitems, lane, va, ka, win, tail, cend, run);
+        if (gi + 1 >= ngroups) { retire_group(vb); break; }
+        issue_group(gi + 2, nitems, cur, R, lane, fallback, va, ka);
+        consume_group(gi + 1, nitems, lane, vb, kb, win, tail, cend, run);
+        if (gi + 2 >= ngroups) { retire_group(va); break; }
+        issue_group(gi + 3, nitems, cur, R, lane, fallback, vb, kb);
+    }
+#elif defined(ZP_DB)
+    // Double-buffered: the next group is in flight while one is consumed.
+    // Every issue is unconditional (dummies past the end) so both buffers
+    // hold exactly ZP_G loads at the loop header on every path.
+    uint4 vb[ZP_G];
+    uint32_t kb[ZP_G];
+    for (uint32_t gi = 0;; gi += 2) {
+        issue_group(gi + 1, nitems, cur, R, lane, fallback, vb, kb);
+        consume_group(gi, nitems, lane, va, ka, win, tail, cend, run);
+        if (gi + 1 >= ngroups) { retire_group(vb); break; }
+        issue_group(gi + 2, nitems, cur, R, lane, fallback, va, ka);
+        consume_group(gi + 1, nitems, lane, vb, kb, win, tail, cend, run);
+        if (gi + 2 >= ngroups) { retire_group(va); break; }
+    }
+#else
     consume_group(0, nitems, lane, va, ka, win, tail, cend, run);
     for (uint32_t gi = 1; gi < ngroups; ++gi) {
-        issue_group(gi, nitems, pfx, cur, R, lane, fallback, va, ka);
+        issue_group(gi, nitems, cur, R, lane, fallback, va, ka);
         consume_group(gi, nitems, lane, va, ka, win, tail, cend, run);
     }
+#endif
     // LDS written by other lanes of this wave: order the wave's LDS ops.
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
