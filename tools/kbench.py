@@ -64,7 +64,17 @@ def main():
                 print(f"membw read 13 GiB blocks={blocks} nt={nt}: "
                       f"{buf.numel() / (np.median(ms) * 1e-3) / 1e9:.0f} GB/s "
                       f"(min {min(ms):.3f} ms)", flush=True)
-        del buf
+        mb.membw_region.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                    ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p]
+        rout = torch.zeros((13 << 30) // 1024 * 64, dtype=torch.int32, device=dev)
+        for region in (16 << 10, 48 << 10, 192 << 10):
+            for g in (4, 8, 16):
+                ms = time_launches(lambda: mb.membw_region(buf.data_ptr(), buf.numel(),
+                                                           rout.data_ptr(), region, g, None), 10)
+                nbytes = buf.numel() // region * region
+                print(f"membw region={region >> 10}KiB G={g}: "
+                      f"{nbytes / (np.median(ms) * 1e-3) / 1e9:.0f} GB/s", flush=True)
+        del buf, rout
         torch.cuda.empty_cache()
     for cfg in args.configs.split(","):
         n = sizes[cfg]

@@ -36,3 +36,46 @@ extern "C" int membw_read(const void* p, uint64_t bytes, uint32_t* out, int bloc
                             (const uint4*)p, n16, out);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+
+// Region pattern (the parse kernel's): each wave streams its own contiguous
+// region in 1 KiB wave-wide loads, G loads per round trip (static count),
+// 4 waves per workgroup, one wave per region.
+template <int G>
+__global__ void __launch_bounds__(256) read_region(const uint8_t* __restrict__ p, uint64_t region,
+                                                   uint64_t nreg, uint32_t* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t w = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (w >= nreg) return;
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    const uint8_t* base = p + w * region;
+    const uint64_t items = region / 1024;
+    uint32_t acc = 0;
+    for (uint64_t i = 0; i < items; i += G) {
+        u32x4 v[G];
+#pragma unroll
+        for (int q = 0; q < G; ++q) {
+            const uint64_t it = i + q < items ? i + q : items - 1;
+            v[q] = __builtin_nontemporal_load(
+                (const __attribute__((address_space(1))) u32x4*)(base + it * 1024 + lane * 16));
+        }
+#pragma unroll
+        for (int q = 0; q < G; ++q) acc += v[q].x ^ v[q].y ^ v[q].z ^ v[q].w;
+    }
+    out[w * 64 + lane] = acc;
+}
+
+extern "C" int membw_region(const void* p, uint64_t bytes, uint32_t* out, uint64_t region, int g,
+                            void* stream) {
+    const uint64_t nreg = bytes / region;
+    const unsigned blocks = (unsigned)((nreg + 3) / 4);
+    switch (g) {
+    case 4: hipLaunchKernelGGL(read_region<4>, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                               (const uint8_t*)p, region, nreg, out); break;
+    case 8: hipLaunchKernelGGL(read_region<8>, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                               (const uint8_t*)p, region, nreg, out); break;
+    case 16: hipLaunchKernelGGL(read_region<16>, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                                (const uint8_t*)p, region, nreg, out); break;
+    default: return -1;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}

@@ -45,10 +45,14 @@
 #include "../../include/zero_packet.h"
 #include "../../include/zero_packet_errstr.h"
 
-#define ZP_WIN 128           // window bytes per frame
+#ifndef ZP_WIN
+#define ZP_WIN 128           // LDS header window bytes per frame (multiple of 16)
+#endif
 #define ZP_WIN_CH (ZP_WIN / 16)
 #define ZP_GIANT 65536u      // frames longer than this take the exact path
+#ifndef ZP_WAVES
 #define ZP_WAVES 4           // waves per workgroup
+#endif
 #ifndef ZP_G
 #define ZP_G 8               // stream items (1 KiB loads) per group
 #endif
@@ -98,7 +102,6 @@ __device__ __forceinline__ uint4 ldg16(uintptr_t a) {
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 __device__ __forceinline__ uint32_t ldg4(uintptr_t a) { return *(const ZP_GLOBAL uint32_t*)a; }
-__device__ __forceinline__ uint32_t ldg1(uintptr_t a) { return *(const ZP_GLOBAL uint8_t*)a; }
 
 // Streamed 16-B chunk, read once: nontemporal.
 __device__ __forceinline__ uint4 ld_stream(uintptr_t a) {
@@ -174,6 +177,8 @@ struct FrameView {
     uint32_t shift;          // frame address & 15 (window starts 16-aligned)
     uint32_t wlen;           // frame bytes available in the window
     uint32_t len;            // frame length
+    uint4 xc;                // past the window: one cached 16-B chunk ...
+    uint32_t xi;             // ... and its index from A & ~15 (~0: none)
 };
 
 __device__ __forceinline__ uint4 win_chunk(const FrameView& f, uint32_t c) {
@@ -184,16 +189,29 @@ __device__ __forceinline__ uint32_t win_dw(const FrameView& f, uint32_t d) {
     return ((const uint32_t*)&f.win[c * 64 + (f.lane ^ c)])[d & 3];
 }
 
-__device__ __forceinline__ uint32_t rd8(const FrameView& f, uint32_t x) {
-    if (x < f.wlen) {
-        uint32_t y = x + f.shift;
-        return (win_dw(f, y >> 2) >> ((y & 3) * 8)) & 0xFFu;
+// Chunk c (from A & ~15) past the window: one 16-B load per distinct chunk
+// (deep IPv6 extension chains and IP-in-IP read a few bytes each from the
+// same chunks).
+__device__ __forceinline__ uint4 fb_chunk(FrameView& f, uint32_t c) {
+    if (c != f.xi) {
+        f.xc = ldg16(((uintptr_t)f.g & ~(uintptr_t)15) + 16u * c);
+        f.xi = c;
     }
-    return ldg1((uintptr_t)f.g + x);
+    return f.xc;
+}
+
+__device__ __forceinline__ uint32_t dw_of(uint4 v, uint32_t d) {
+    return d == 0 ? v.x : d == 1 ? v.y : d == 2 ? v.z : v.w;
+}
+
+__device__ __forceinline__ uint32_t rd8(FrameView& f, uint32_t x) {
+    const uint32_t y = x + f.shift;
+    const uint32_t dw = x < f.wlen ? win_dw(f, y >> 2) : dw_of(fb_chunk(f, y >> 4), (y >> 2) & 3);
+    return (dw >> ((y & 3) * 8)) & 0xFFu;
 }
 
 // Big-endian 16-bit field at frame offset x.
-__device__ __forceinline__ uint32_t rd16(const FrameView& f, uint32_t x) {
+__device__ __forceinline__ uint32_t rd16(FrameView& f, uint32_t x) {
     if (x + 1 < f.wlen) {
         const uint32_t y = x + f.shift, d = y >> 2;
         const uint32_t lo = win_dw(f, d);
@@ -205,7 +223,7 @@ __device__ __forceinline__ uint32_t rd16(const FrameView& f, uint32_t x) {
 }
 
 // Arena-parity word sum V of frame bytes [lo, hi) (both <= len).
-__device__ uint32_t sumV(const FrameView& f, uint32_t lo, uint32_t hi) {
+__device__ uint32_t sumV(FrameView& f, uint32_t lo, uint32_t hi) {
     uint32_t s = 0;
     const uint32_t h1 = hi < f.wlen ? hi : f.wlen;
     if (lo < h1) {
@@ -219,11 +237,12 @@ __device__ uint32_t sumV(const FrameView& f, uint32_t lo, uint32_t hi) {
     }
     const uint32_t l2 = lo > f.wlen ? lo : f.wlen;
     if (l2 < hi) {
-        const uintptr_t a0 = (uintptr_t)f.g + l2, a1 = (uintptr_t)f.g + hi;
-        for (uintptr_t d = a0 & ~(uintptr_t)3; d < a1; d += 4) {
-            const int l = a0 > d ? (int)(a0 - d) : 0;
-            const int h = a1 - d < 4 ? (int)(a1 - d) : 4;
-            s = sad16(ldg4(d) & byte_mask(0, l, h), s);
+        const int ylo = (int)(l2 + f.shift), yhi = (int)(hi + f.shift);
+        const int c0 = ylo >> 4, c1 = (yhi - 1) >> 4;
+        for (int c = c0; c <= c1; ++c) {
+            const int l = c == c0 ? ylo - 16 * c : 0;
+            const int h = c == c1 ? yhi - 16 * c : 16;
+            s = chunk_sum(fb_chunk(f, (uint32_t)c), l, h, s);
         }
     }
     return s;
@@ -236,7 +255,7 @@ __device__ __forceinline__ uint32_t sum_head(const FrameView& f) {
 
 // Exact big-endian word sum (reference parity: words start at lo) of frame
 // bytes [lo, hi): split into even/odd-offset byte sums.
-__device__ uint32_t sumW_exact(const FrameView& f, uint32_t lo, uint32_t hi) {
+__device__ uint32_t sumW_exact(FrameView& f, uint32_t lo, uint32_t hi) {
     uint32_t E = 0, O = 0;
     for (uint32_t x = lo; x < hi; x += 4) {
         uint32_t v;
@@ -290,7 +309,7 @@ struct Walk {
 
 // Extension-header walk (headers.rs:51-213). Returns 0 or a zp_err.
 // pos = IPv6 payload start; outputs slot offsets relative to pos.
-__device__ int ext_walk(const FrameView& f, uint32_t pos, uint32_t nh,
+__device__ int ext_walk(FrameView& f, uint32_t pos, uint32_t nh,
                         uint32_t* present, uint16_t off[6], uint32_t* total,
                         uint32_t* final_nh) {
     uint32_t pres = 0, tot = 0, fin = 0;
@@ -348,7 +367,7 @@ __device__ int ext_walk(const FrameView& f, uint32_t pos, uint32_t nh,
     return 0;
 }
 
-__device__ void walk_frame(const FrameView& f, Walk& w) {
+__device__ void walk_frame(FrameView& f, Walk& w) {
     zp_record& r = w.rec;
     w.pending = 0; w.acc = 0; w.l4 = 0; w.v6 = 0;
     const uint32_t len = f.len;
@@ -765,6 +784,8 @@ zp_parse_kernel(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ 
     fv.shift = shift;
     fv.len = len;
     fv.wlen = wlen;
+    fv.xc = make_uint4(0, 0, 0, 0);
+    fv.xi = ~0u;
     Walk w;
     w.rec = zp_record{};
     w.inner = zp_ext_offsets{};
