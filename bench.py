@@ -139,14 +139,25 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    ndev = torch.cuda.device_count()
+    # One rank per GPU over RCCL. More ranks than GPUs (a rehearsal of the N>1
+    # path on a smaller box) share devices and synchronise over gloo.
+    shared = world > ndev
+    local_dev = local % ndev if shared else local
+    torch.cuda.set_device(local_dev)
+    dev = torch.device("cuda", local_dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if shared:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     def barrier():
         if world > 1:
-            dist.barrier(device_ids=[local])
+            if shared:
+                dist.barrier()
+            else:
+                dist.barrier(device_ids=[local_dev])
 
     zp = importlib.import_module("zero-packet_amd")
     n = args.packets or DEFAULT_PACKETS[args.config]
@@ -179,7 +190,7 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     kms = [a.elapsed_time(b) for a, b in ev]
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if shared else dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
@@ -201,7 +212,8 @@ def main():
         "config": {"workload": WORKLOADS[args.config], "config": args.config,
                    "frames_per_gpu": n, "bytes_per_gpu": total_bytes,
                    "mean_frame_bytes": round(total_bytes / n, 2),
-                   "parallelism": f"dp{world} (independent shards, no collective)"},
+                   "parallelism": f"dp{world} (independent shards, no collective)"
+                                  + (" [ranks share GPUs: rehearsal only]" if shared else "")},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "traffic_source": traffic_src,

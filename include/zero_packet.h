@@ -177,6 +177,14 @@ void    zp_ctx_destroy(zp_ctx* ctx);
 int zp_parse_batch_host(zp_ctx* ctx, const uint8_t* arena, uint64_t arena_bytes,
                         const uint64_t* offs, const uint32_t* lens, uint64_t n,
                         zp_record* records, zp_ext_offsets* inner_ext);
+/* The same over several devices (one context each, e.g. the 8 GPUs of a
+ * node): contiguous frame ranges with balanced byte totals run concurrently,
+ * one host thread per context. No cross-device exchange. Returns 0 or the
+ * first failing context's code (zp_last_error() names the context). */
+int zp_parse_batch_host_multi(zp_ctx* const* ctxs, int nctx, const uint8_t* arena,
+                              uint64_t arena_bytes, const uint64_t* offs,
+                              const uint32_t* lens, uint64_t n, zp_record* records,
+                              zp_ext_offsets* inner_ext);
 /* One frame through the GPU path (PacketParser::parse equivalent).
  * Returns the zp_err code (>= 0) or a negative value on HIP failure. */
 int zp_parse_one(zp_ctx* ctx, const uint8_t* frame, uint64_t len,

@@ -416,6 +416,19 @@ private:
     zp_ctx* ctx_;
 };
 
+// A host batch over several devices (one Context each): byte-balanced
+// contiguous ranges, concurrently (zp_parse_batch_host_multi).
+inline void parse_batch_multi(Context* const* ctxs, int nctx, const uint8_t* arena,
+                              uint64_t arena_bytes, const uint64_t* offs, const uint32_t* lens,
+                              uint64_t n, zp_record* records, zp_ext_offsets* inner_ext = nullptr) {
+    zp_ctx* raw[64];
+    if (nctx < 1 || nctx > 64) throw std::invalid_argument("parse_batch_multi: 1..64 contexts");
+    for (int d = 0; d < nctx; ++d) raw[d] = ctxs[d]->get();
+    if (zp_parse_batch_host_multi(raw, nctx, arena, arena_bytes, offs, lens, n, records,
+                                  inner_ext) < 0)
+        throw std::runtime_error(std::string("zp_parse_batch_host_multi: ") + zp_last_error());
+}
+
 // Device-resident batch (the hot path): enqueue on a hipStream_t (void*).
 inline void parse_batch_device(const uint8_t* arena, const uint64_t* offs, const uint32_t* lens,
                                uint64_t n, zp_record* records, zp_ext_offsets* inner_ext,

@@ -249,6 +249,27 @@ def test_host_path(zp, golden, pinned):
     assert_same(rec, ext, want, wext)
 
 
+def test_host_path_multi(zp, golden):
+    """zp_parse_batch_host_multi: byte-balanced ranges over several contexts
+    (here 3 contexts sharing device 0), concurrently, results in place."""
+    frames = fuzz_frames(zp, golden, 15000, 23)
+    arena, offs, lens = pack(frames)
+    lib = zp._lib.hip()
+    ctxs = [lib.zp_ctx_create(0, 1 << 20) for _ in range(3)]
+    assert all(ctxs)
+    arr = (ctypes.c_void_p * 3)(*ctxs)
+    rec = np.zeros(len(offs), zp.records.RECORD_DTYPE)
+    ext = np.zeros(len(offs), zp.records.EXT_DTYPE)
+    rc = lib.zp_parse_batch_host_multi(arr, 3, arena.ctypes.data, len(arena), offs.ctypes.data,
+                                       lens.ctypes.data, len(offs), rec.ctypes.data,
+                                       ext.ctypes.data)
+    for c in ctxs:
+        lib.zp_ctx_destroy(c)
+    assert rc == 0, lib.zp_last_error()
+    want, wext = orc.parse_batch(arena, offs, lens)
+    assert_same(rec, ext, want, wext)
+
+
 # ---- full-size C3 properties ----------------------------------------------
 
 def test_full_size_c3_properties(zp):

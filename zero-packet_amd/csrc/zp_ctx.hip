@@ -15,6 +15,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <pthread.h>
+
 #include "../../include/zero_packet.h"
 
 // Thread-local error text shared with zp_parse.hip (read via zp_last_error()).
@@ -226,4 +228,83 @@ extern "C" int zp_parse_one(zp_ctx* c, const uint8_t* frame, uint64_t len,
     int rc = zp_parse_batch_host(c, frame, len, &off, &l, 1, record, inner_ext);
     if (rc) return rc;
     return record->err;
+}
+
+// Several devices at once (one context each): the batch is cut into
+// contiguous frame ranges with balanced byte totals, one per context, and the
+// contexts run concurrently on their own host threads (the
+// frames are independent, there is no exchange step). Results land in the
+// caller's arrays at the frames' own indices. Plain pthreads: no C++ runtime
+// objects cross the library boundary (the host process may carry another
+// libstdc++).
+struct MultiJob {
+    zp_ctx* ctx;
+    const uint8_t* arena;
+    uint64_t arena_bytes;
+    const uint64_t* offs;
+    const uint32_t* lens;
+    uint64_t n;
+    zp_record* recs;
+    zp_ext_offsets* ext;
+    int rc;
+    char err[ERRBUF_LEN];
+};
+
+static void* multi_worker(void* p) {
+    MultiJob* j = (MultiJob*)p;
+    j->rc = zp_parse_batch_host(j->ctx, j->arena, j->arena_bytes, j->offs, j->lens, j->n,
+                                j->recs, j->ext);
+    if (j->rc) snprintf(j->err, ERRBUF_LEN, "%s", g_ctx_error);
+    return NULL;
+}
+
+extern "C" int zp_parse_batch_host_multi(zp_ctx* const* ctxs, int nctx, const uint8_t* arena,
+                                         uint64_t arena_bytes, const uint64_t* offs,
+                                         const uint32_t* lens, uint64_t n, zp_record* recs,
+                                         zp_ext_offsets* ext) {
+    if (!ctxs || nctx < 1 || nctx > 256) return -1;
+    for (int d = 0; d < nctx; ++d)
+        if (!ctxs[d]) return -1;
+    if (n == 0) return 0;
+    if (!arena || !offs || !lens || !recs) return -1;
+    uint64_t total = 0;
+    for (uint64_t i = 0; i < n; ++i) total += lens[i];
+    MultiJob* jobs = (MultiJob*)calloc((size_t)nctx, sizeof(MultiJob));
+    pthread_t* th = (pthread_t*)calloc((size_t)nctx, sizeof(pthread_t));
+    char* started = (char*)calloc((size_t)nctx, 1);
+    if (!jobs || !th || !started) {
+        free(jobs); free(th); free(started);
+        snprintf(g_ctx_error, ERRBUF_LEN, "zp_parse_batch_host_multi: out of memory");
+        return -1;
+    }
+    // range d = frames whose exclusive byte prefix lies in [total*d/nctx, total*(d+1)/nctx)
+    uint64_t acc = 0, i = 0;
+    for (int d = 0; d < nctx; ++d) {
+        const uint64_t lo = i;
+        const uint64_t target = d + 1 == nctx ? ~0ull
+                              : (uint64_t)((unsigned __int128)total * (unsigned)(d + 1) / (unsigned)nctx);
+        while (i < n && acc < target) acc += lens[i++];
+        jobs[d] = MultiJob{ctxs[d], arena, arena_bytes, offs + lo, lens + lo, i - lo, recs + lo,
+                           ext ? ext + lo : NULL, 0, {0}};
+    }
+    int rc = 0;
+    for (int d = 0; d < nctx; ++d) {
+        if (jobs[d].n == 0) continue;
+        if (pthread_create(&th[d], NULL, multi_worker, &jobs[d]) == 0) {
+            started[d] = 1;
+        } else {
+            multi_worker(&jobs[d]);               // no thread: run it here
+        }
+    }
+    for (int d = 0; d < nctx; ++d)
+        if (started[d]) pthread_join(th[d], NULL);
+    for (int d = 0; d < nctx; ++d) {
+        if (jobs[d].rc) {
+            snprintf(g_ctx_error, ERRBUF_LEN, "device context %d: %s", d, jobs[d].err);
+            rc = jobs[d].rc;
+            break;
+        }
+    }
+    free(jobs); free(th); free(started);
+    return rc;
 }

@@ -51,10 +51,13 @@
 #define ZP_WIN_CH (ZP_WIN / 16)
 #define ZP_GIANT 65536u      // frames longer than this take the exact path
 #ifndef ZP_WAVES
-#define ZP_WAVES 4           // waves per workgroup
+#define ZP_WAVES 1           // waves per workgroup (independent waves; 1 = finest LDS granularity)
 #endif
 #ifndef ZP_G
 #define ZP_G 8               // stream items (1 KiB loads) per group
+#endif
+#ifndef ZP_G0
+#define ZP_G0 ZP_G           // items of a tile's first group (issued before the previous walk)
 #endif
 // Timing-only ablations (tools/build_variants.sh); never set in the product:
 //   ZP_ABL_FAKE_WALK  replace the walk by "pending L4 at offset 42"
@@ -564,8 +567,6 @@ __device__ __forceinline__ uint32_t bperm(uint32_t v, uint32_t r) {
     return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(r << 2), (int)v);
 }
 
-// Always issues exactly ZP_G loads (items past the end re-read the wave's
-// last chunk): a static load count keeps the compiler's s_waitcnt exact.
 // Rebuilds the start masks of items [w0, w0 + 64): one LDS atomic OR per
 // frame starting there. Straight-line code (no loop): a loop here would make
 // LLVM's wait-count insertion drain the group in flight (vmcnt(0)).
@@ -584,15 +585,17 @@ __device__ __forceinline__ void build_starts(uint32_t w0, const Cursor& c, const
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Always issues exactly ZP_G loads (items past the end re-read the wave's
-// last chunk): a static load count keeps the compiler's s_waitcnt exact.
-__device__ __forceinline__ void issue_group(uint32_t g, uint32_t nitems, Cursor& c,
+// Always issues exactly G loads (items past the end re-read the wave's last
+// chunk, or a dummy): a static load count keeps the compiler's s_waitcnt
+// exact.
+template <int G>
+__device__ __forceinline__ void issue_group(uint32_t i0, uint32_t nitems, Cursor& c,
                                             const Ranked& R, int lane, uintptr_t fallback,
-                                            uint4 (&v)[ZP_G], uint32_t (&keep)[ZP_G]) {
-    uintptr_t a[ZP_G];
+                                            uint4 (&v)[G], uint32_t (&keep)[G]) {
+    uintptr_t a[G];
 #pragma unroll
-    for (int q = 0; q < ZP_G; ++q) {
-        const uint32_t i = g * ZP_G + q;
+    for (int q = 0; q < G; ++q) {
+        const uint32_t i = i0 + q;
         const uint32_t base = 64u * i;
         if ((i & 63u) == 0 && i < nitems) build_starts(i, c, R, lane);   // wave-uniform
         uint64_t F = 0;
@@ -620,7 +623,7 @@ __device__ __forceinline__ void issue_group(uint32_t g, uint32_t nitems, Cursor&
     }
 #ifndef ZP_ABL_STREAM_OFF
 #pragma unroll
-    for (int q = 0; q < ZP_G; ++q) v[q] = ld_stream(a[q]);
+    for (int q = 0; q < G; ++q) v[q] = ld_stream(a[q]);
 #endif
     // Compiler barrier: keeps LLVM from sinking the loads below the consume
     // of the previous group (which would serialise the double buffer).
@@ -629,18 +632,20 @@ __device__ __forceinline__ void issue_group(uint32_t g, uint32_t nitems, Cursor&
 
 // An empty asm that reads every register of the group: forces the wait for
 // all of its loads at this point.
-__device__ __forceinline__ void retire_group(const uint4 (&v)[ZP_G]) {
+template <int G>
+__device__ __forceinline__ void retire_group(const uint4 (&v)[G]) {
 #pragma unroll
-    for (int q = 0; q < ZP_G; ++q) asm volatile("" ::"v"(v[q].x), "v"(v[q].y), "v"(v[q].z), "v"(v[q].w));
+    for (int q = 0; q < G; ++q) asm volatile("" ::"v"(v[q].x), "v"(v[q].y), "v"(v[q].z), "v"(v[q].w));
 }
 
-__device__ __forceinline__ void consume_group(uint32_t g, uint32_t nitems, int lane,
-                                              const uint4 (&v)[ZP_G], const uint32_t (&keep)[ZP_G],
+template <int G>
+__device__ __forceinline__ void consume_group(uint32_t i0, uint32_t nitems, int lane,
+                                              const uint4 (&v)[G], const uint32_t (&keep)[G],
                                               uint4* win, uint4* tail, uint32_t* cend,
                                               uint32_t& run) {
 #pragma unroll
-    for (int q = 0; q < ZP_G; ++q) {
-        const uint32_t i = g * ZP_G + q;
+    for (int q = 0; q < G; ++q) {
+        const uint32_t i = i0 + q;
         if (i >= nitems) break;                               // wave-uniform
         const uint32_t k = keep[q];
         if (k & KEEP_WIN) win[k & 0x1FFu] = v[q];
@@ -663,155 +668,107 @@ __device__ __forceinline__ void consume_group(uint32_t g, uint32_t nitems, int l
 // --------------------------------------------------------------------------
 // The batch kernel.
 // --------------------------------------------------------------------------
-__global__ void __launch_bounds__(64 * ZP_WAVES)
-zp_parse_kernel(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs,
-                const uint32_t* __restrict__ lens, uint64_t n,
-                zp_record* __restrict__ records, zp_ext_offsets* __restrict__ inner_ext) {
-    // Per wave: header windows [8][64] + last chunks [64] (16-B cells), and
-    // the stream's running sum at each frame's last chunk.
-    __shared__ uint4 win_all[ZP_WAVES][(ZP_WIN_CH + 1) * 64];
-    __shared__ uint32_t cend_all[ZP_WAVES][64];
-    __shared__ uint64_t starts_all[ZP_WAVES][64];
-    const int lane = threadIdx.x & 63;
-    const int wid = threadIdx.x >> 6;
-    const uint64_t f0 = ((uint64_t)blockIdx.x * ZP_WAVES + wid) * 64;
-    if (f0 >= n) return;                       // whole wave past the batch (uniform)
-#ifdef ZP_STAMPS
-    const uint64_t wave_id = f0 / 64;
-#endif
-    STAMP(0);
-    const uint64_t p = f0 + lane;
-    const bool live = p < n;
-    const uint32_t len = live ? lens[p] : 0;
-    const uint8_t* g = arena + (live ? offs[p] : 0);
-    const uintptr_t ga = (uintptr_t)g;
-    uint4* win = &win_all[wid][0];
-    uint4* tail = &win_all[wid][ZP_WIN_CH * 64];
-    uint32_t* cend = &cend_all[wid][0];
-#ifdef ZP_STAMPS
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
-    STAMP(1);
+// One tile = 64 consecutive frames on one wave (lane = frame).
+struct WaveLds {
+    uint4 win[(ZP_WIN_CH + 1) * 64];   // header windows [ZP_WIN_CH][64] + last chunks [64]
+    uint32_t cend[64];                  // running stream sum at each frame's last chunk
+    uint64_t starts[64];                // per-item frame-start masks
+};
 
-    // ---- stream setup: chunks [A & ~15, E) of frames of 64 B .. 64 KiB;
-    // longer frames stream their window only (exact checksum path).
-    const uint32_t shift = (uint32_t)(ga & 15);
-    const uint32_t wlen = len < ZP_WIN - shift ? len : ZP_WIN - shift;
-    const bool giant = len > ZP_GIANT;
-    const uint32_t span = giant ? (uint32_t)ZP_WIN : len + shift;
+struct TileState {
+    uint64_t tile;
+    uintptr_t ga;            // this lane's frame
+    uint32_t len, shift, wlen, rank;
+    bool live, giant;
+    uint32_t nitems;         // wave-uniform
+    Ranked R;
+    Cursor cur;
+    uint32_t run;            // running stream sum
+};
+
+// Chunk ranges, ranks and the compacted per-rank frame table of a tile.
+// len = 0 lanes (past the batch) own no chunks.
+__device__ __forceinline__ void tile_setup(TileState& s, uint64_t tile, uint32_t len,
+                                           uintptr_t ga, uint64_t n, int lane, WaveLds& lds) {
+    s.tile = tile;
+    s.ga = ga;
+    s.len = len;
+    s.live = tile * 64 + lane < n;
+    // chunks [A & ~15, E) of frames of 64 B .. 64 KiB; longer frames stream
+    // their window only (exact checksum path)
+    s.shift = (uint32_t)(ga & 15);
+    s.wlen = len < ZP_WIN - s.shift ? len : ZP_WIN - s.shift;
+    s.giant = len > ZP_GIANT;
+    const uint32_t span = s.giant ? (uint32_t)ZP_WIN : len + s.shift;
     const uint32_t nch = len >= 64 ? (span + 15) >> 4 : 0u;
     const uint64_t M = __ballot(nch > 0);
-    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(M >> 32),
-                              __builtin_amdgcn_mbcnt_lo((uint32_t)M, 0u));
+    s.rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(M >> 32),
+                                       __builtin_amdgcn_mbcnt_lo((uint32_t)M, 0u));
     const uint32_t incl = wave_scan(nch);
     const uint32_t pfx = incl - nch;
     const uint32_t T = rdl(incl, 63);
-    const uint32_t nitems = (T + 63) >> 6;
-    const uint32_t ngroups = (nitems + ZP_G - 1) / ZP_G;
-    Ranked R;
-    {   // compact the non-empty frames into rank order (tail cells as scratch)
-        const uintptr_t org = (ga & ~(uintptr_t)15) - 16ull * pfx;
-        if (nch) tail[rank] = make_uint4((uint32_t)org, (uint32_t)(org >> 32), incl - 1, pfx);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const uint4 t = tail[lane];            // lanes >= popcount(M): never selected
-        R.org_lo = t.x; R.org_hi = t.y; R.last = t.z; R.pfx = t.w;
-    }
-    Cursor cur;
-    cur.rbase = ~0u;
-    cur.nz = (uint32_t)__builtin_popcountll(M);
-    cur.starts = &starts_all[wid][0];
-    const uintptr_t fallback = (uintptr_t)&zp_safe_chunk;   // only when T == 0
+    s.nitems = (T + 63) >> 6;
+    // compact the non-empty frames into rank order (ds_permute: LDS untouched)
+    const uint32_t nz = (uint32_t)__builtin_popcountll(M);
+    const uint32_t dst = nch ? s.rank : nz + ((uint32_t)lane - s.rank);
+    const uintptr_t org = (ga & ~(uintptr_t)15) - 16ull * pfx;
+    const int a = (int)(dst << 2);
+    s.R.org_lo = (uint32_t)__builtin_amdgcn_ds_permute(a, (int)(uint32_t)org);
+    s.R.org_hi = (uint32_t)__builtin_amdgcn_ds_permute(a, (int)(uint32_t)(org >> 32));
+    s.R.last = (uint32_t)__builtin_amdgcn_ds_permute(a, (int)(incl - 1));
+    s.R.pfx = (uint32_t)__builtin_amdgcn_ds_permute(a, (int)pfx);
+    s.cur.rbase = ~0u;
+    s.cur.nz = nz;
+    s.cur.starts = &lds.starts[0];
+    s.run = 0;
+}
 
-    // ---- C. stream (+ windows and last chunks into LDS): one group of ZP_G
-    // items per iteration; no load is in flight across the loop back-edge.
-    uint4 va[ZP_G];
-    uint32_t ka[ZP_G];
-    uint32_t run = 0;
-    issue_group(0, nitems, cur, R, lane, fallback, va, ka);
-    // The compaction reads of `tail` must land before the stream overwrites it.
+__device__ __forceinline__ void wave_lds_fence() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    STAMP(2);
-#if defined(ZP_DB2)
-    // Double-buffered, both groups issued ahead: each iteration consumes a
-    // group and immediately re-issues into the registers it just drained.
-    uint4 vb[ZP_G];
-    uint32_t kb[ZP_G];
-    issue_group(1, nitems, cur, R, lane, fallback, vb, kb);
-    for (uint32_t gi = 0;; gi += 2) {
-        consume_group(gi, nitems, lane, va, ka, win, tail, cend, run);
-        if (gi + 1 >= ngroups) { retire_group(vb); break; }
-        issue_group(gi + 2, nitems, cur, R, lane, fallback, va, ka);
-        consume_group(gi + 1, nitems, lane, vb, kb, win, tail, cend, run);
-        if (gi + 2 >= ngroups) { retire_group(va); break; }
-        issue_group(gi + 3, nitems, cur, R, lane, fallback, vb, kb);
-    }
-#elif defined(ZP_DB)
-    // Double-buffered: the next group is in flight while one is consumed.
-    // Every issue is unconditional (dummies past the end) so both buffers
-    // hold exactly ZP_G loads at the loop header on every path.
-    uint4 vb[ZP_G];
-    uint32_t kb[ZP_G];
-    for (uint32_t gi = 0;; gi += 2) {
-        issue_group(gi + 1, nitems, cur, R, lane, fallback, vb, kb);
-        consume_group(gi, nitems, lane, va, ka, win, tail, cend, run);
-        if (gi + 1 >= ngroups) { retire_group(vb); break; }
-        issue_group(gi + 2, nitems, cur, R, lane, fallback, va, ka);
-        consume_group(gi + 1, nitems, lane, vb, kb, win, tail, cend, run);
-        if (gi + 2 >= ngroups) { retire_group(va); break; }
-    }
-#else
-    consume_group(0, nitems, lane, va, ka, win, tail, cend, run);
-    for (uint32_t gi = 1; gi < ngroups; ++gi) {
-        issue_group(gi, nitems, cur, R, lane, fallback, va, ka);
-        consume_group(gi, nitems, lane, va, ka, win, tail, cend, run);
-    }
-#endif
-    // LDS written by other lanes of this wave: order the wave's LDS ops.
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    STAMP(3);
+}
 
-    // ---- B. walk (lane per frame; the window is indexed by rank)
+// Header walk + checksum verdict + record store of a streamed tile.
+__device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, WaveLds& lds,
+                                            zp_record* __restrict__ records,
+                                            zp_ext_offsets* __restrict__ inner_ext) {
+    uint4* tail = &lds.win[ZP_WIN_CH * 64];
+    const uint8_t* g = (const uint8_t*)s.ga;
     FrameView fv;
-    fv.win = win;
+    fv.win = &lds.win[0];
     fv.g = g;
-    fv.lane = rank & 63u;
-    fv.shift = shift;
-    fv.len = len;
-    fv.wlen = wlen;
+    fv.lane = s.rank & 63u;
+    fv.shift = s.shift;
+    fv.len = s.len;
+    fv.wlen = s.wlen;
     fv.xc = make_uint4(0, 0, 0, 0);
     fv.xi = ~0u;
     Walk w;
     w.rec = zp_record{};
     w.inner = zp_ext_offsets{};
 #ifdef ZP_ABL_FAKE_WALK
-    w.pending = live && len >= 64;
+    w.pending = s.live && s.len >= 64;
     w.l4 = 42; w.acc = 0; w.v6 = 0;
     w.rec.flags = ZP_F_ETHERNET;
 #else
-    if (live) walk_frame(fv, w);
+    if (s.live) walk_frame(fv, w);
     else w.pending = 0;
 #endif
-    STAMP(4);
-
-    // ---- D. verdict + store. The frame's stream sum covers the whole chunks
-    // [A & ~15, E16): L4 sum = that - V[A & ~15, A + l4) - V[E, E16).
-    if (!live) return;
+    if (!s.live) return;
+    // The frame's stream sum covers the whole chunks [A & ~15, E16):
+    // L4 sum = that - V[A & ~15, A + l4) - V[E, E16).
     zp_record rec = w.rec;
     if (w.pending) {
         bool ok;
-        if (giant) {
-            ok = csum_ok_exact(g, w.l4, len, w.acc);
+        if (s.giant) {
+            ok = csum_ok_exact(g, w.l4, s.len, w.acc);
         } else {
-            const bool odd = (ga + w.l4) & 1;
-            const uint32_t fsum = cend[rank] - (rank ? cend[rank - 1] : 0u);
-            const uint32_t he = (len + shift) & 15u;      // bytes of the last chunk in use
-            const uint32_t ex = he ? range_sum(tail[rank], he, 16u) : 0u;
+            const bool odd = (s.ga + w.l4) & 1;
+            const uint32_t r = s.rank;
+            const uint32_t fsum = lds.cend[r] - (r ? lds.cend[r - 1] : 0u);
+            const uint32_t he = (s.len + s.shift) & 15u;    // bytes of the last chunk in use
+            const uint32_t ex = he ? range_sum(tail[r], he, 16u) : 0u;
             ok = csum_ok(w.acc, fsum - sumV(fv, 0, w.l4) - sum_head(fv) - ex, odd);
         }
         if (!ok) {
@@ -819,18 +776,120 @@ zp_parse_kernel(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ 
             rec.err = (uint8_t)(w.v6 ? ZP_ERR_IPV6_L4_CHECKSUM : ZP_ERR_IPV4_L4_CHECKSUM);
         }
     }
-    STAMP(5);
     uint4 q2[2];
     memcpy(q2, &rec, sizeof rec);
+    const uint64_t p = s.tile * 64 + lane;
     uint4* dst = (uint4*)(records + p);
     dst[0] = q2[0];
     dst[1] = q2[1];
     if (inner_ext && (rec.flags & ZP_F_INNER_EXT)) inner_ext[p] = w.inner;
 }
 
-// --------------------------------------------------------------------------
-// C ABI
-// --------------------------------------------------------------------------
+// Descriptor loads are unconditional (clamped index, masked after): a load
+// count that depends on the lane's branch turns later waits into vmcnt(0).
+__device__ __forceinline__ void load_desc(const uint8_t* arena, const uint64_t* offs,
+                                          const uint32_t* lens, uint64_t n, uint64_t tile,
+                                          int lane, uint32_t& len, uintptr_t& ga) {
+    const uint64_t p = tile * 64 + lane;
+    const uint64_t pc = p < n ? p : n - 1;
+    const uint32_t l = lens[pc];
+    const uint64_t o = offs[pc];
+    len = p < n ? l : 0u;
+    ga = (uintptr_t)arena + (p < n ? o : 0);
+}
+
+// Persistent grid: wave gw handles tiles gw, gw + W, ... (W = all waves of
+// the grid, sized to the resident capacity by the launcher). Per tile:
+//   descriptors of the next tile      (loads, land during this tile's stream)
+//   stream groups 1..                 (group 0 was issued and consumed before)
+//   setup + issue of the next tile's group 0   } ZP_OVERLAP: the next tile's
+//   walk + verdict of this tile                } first loads fly during the walk
+//   consume of the next tile's group 0
+// No load is in flight across the loop back-edge (see issue_group).
+__global__ void __launch_bounds__(64 * ZP_WAVES)
+zp_parse_kernel(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs,
+                const uint32_t* __restrict__ lens, uint64_t n,
+                zp_record* __restrict__ records, zp_ext_offsets* __restrict__ inner_ext) {
+    __shared__ WaveLds lds_all[ZP_WAVES];
+    const int lane = threadIdx.x & 63;
+    const int wid = threadIdx.x >> 6;
+    WaveLds& lds = lds_all[wid];
+    const uint64_t ntiles = (n + 63) / 64;
+    const uint64_t W = (uint64_t)gridDim.x * ZP_WAVES;
+    uint64_t t = (uint64_t)blockIdx.x * ZP_WAVES + wid;
+    if (t >= ntiles) return;                       // wave-uniform
+    const uintptr_t fallback = (uintptr_t)&zp_safe_chunk;   // dummy loads when T == 0
+    uint4* win = &lds.win[0];
+    uint4* tail = &lds.win[ZP_WIN_CH * 64];
+    uint4 va[ZP_G], v0[ZP_G0];
+    uint32_t ka[ZP_G], k0[ZP_G0];
+    TileState s, sn;
+    {
+        uint32_t len;
+        uintptr_t ga;
+        load_desc(arena, offs, lens, n, t, lane, len, ga);
+        tile_setup(s, t, len, ga, n, lane, lds);
+        issue_group<ZP_G0>(0, s.nitems, s.cur, s.R, lane, fallback, v0, k0);
+        wave_lds_fence();
+        consume_group<ZP_G0>(0, s.nitems, lane, v0, k0, win, tail, lds.cend, s.run);
+    }
+    for (;;) {
+#ifdef ZP_STAMPS
+        const uint64_t wave_id = t;
+#endif
+        STAMP(0);
+        const uint64_t tn = t + W;
+        const bool more = tn < ntiles;             // wave-uniform
+        uint32_t len_n;
+        uintptr_t ga_n;
+        load_desc(arena, offs, lens, n, more ? tn : t, lane, len_n, ga_n);
+        if (!more) len_n = 0;                      // a dummy tile: no chunks, dummy loads
+        STAMP(1);
+        for (uint32_t i0 = ZP_G0; i0 < s.nitems; i0 += ZP_G) {
+            issue_group<ZP_G>(i0, s.nitems, s.cur, s.R, lane, fallback, va, ka);
+            consume_group<ZP_G>(i0, s.nitems, lane, va, ka, win, tail, lds.cend, s.run);
+        }
+        wave_lds_fence();
+        STAMP(2);
+#ifdef ZP_OVERLAP
+        tile_setup(sn, tn, len_n, ga_n, n, lane, lds);
+        issue_group<ZP_G0>(0, sn.nitems, sn.cur, sn.R, lane, fallback, v0, k0);
+        tile_finish(s, n, lane, lds, records, inner_ext);
+#else
+        tile_finish(s, n, lane, lds, records, inner_ext);
+        tile_setup(sn, tn, len_n, ga_n, n, lane, lds);
+        issue_group<ZP_G0>(0, sn.nitems, sn.cur, sn.R, lane, fallback, v0, k0);
+#endif
+        STAMP(3);
+        wave_lds_fence();
+        consume_group<ZP_G0>(0, sn.nitems, lane, v0, k0, win, tail, lds.cend, sn.run);
+        STAMP(4);
+        if (!more) break;
+        s = sn;
+        t = tn;
+    }
+}
+
+// Workgroups of zp_parse_kernel resident at once on the current device (CUs x
+// occupancy), cached per device. 0 = unknown (launch one wave per tile).
+static uint64_t resident_blocks() {
+    static uint64_t cache[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+    if (!cache[dev]) {
+        int per_cu = 0, cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, zp_parse_kernel, 64 * ZP_WAVES, 0)
+                != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            per_cu <= 0 || cus <= 0) {
+            (void)hipGetLastError();
+            return 0;
+        }
+        cache[dev] = (uint64_t)per_cu * (uint64_t)cus;
+    }
+    return cache[dev];
+}
+
 extern "C" int zp_parse_batch_device(const uint8_t* arena, const uint64_t* offs,
                                      const uint32_t* lens, uint64_t n,
                                      zp_record* records, zp_ext_offsets* inner_ext,
@@ -840,11 +899,9 @@ extern "C" int zp_parse_batch_device(const uint8_t* arena, const uint64_t* offs,
         snprintf(g_last_error, sizeof g_last_error, "zp_parse_batch_device: null pointer");
         return -1;
     }
-    const uint64_t blocks = (n + 64 * ZP_WAVES - 1) / (64 * ZP_WAVES);
-    if (blocks > 0x7FFFFFFFull) {
-        snprintf(g_last_error, sizeof g_last_error, "zp_parse_batch_device: batch too large");
-        return -1;
-    }
+    uint64_t blocks = (n + 64 * ZP_WAVES - 1) / (64 * ZP_WAVES);
+    const uint64_t cap = resident_blocks();
+    if (cap && blocks > cap) blocks = cap;       // persistent: waves loop over tiles
     hipLaunchKernelGGL(zp_parse_kernel, dim3((unsigned)blocks), dim3(64 * ZP_WAVES), 0,
                        (hipStream_t)stream, arena, offs, lens, n, records, inner_ext);
     const hipError_t e = hipGetLastError();
