@@ -1,0 +1,41 @@
+"""GPU: bench.py's N>1 path end to end (torch.distributed.run, one process
+per rank). On a one-GPU box the two ranks share cuda:0 and synchronise over
+gloo (bench.py's rehearsal mode); on a multi-GPU node the same command runs
+one rank per GPU over RCCL. Checks the single JSON line: weak scaling, the
+whole-job value, and that each rank parsed its own shard without errors."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_bench_two_ranks():
+    n = 1 << 20
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+           "--config", "c3", "--packets", str(n)]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    r = json.loads(lines[0])
+    assert r["n_gpus"] == 2 and r["scaling"] == "weak" and r["steps"] == 3
+    assert r["config"]["frames_per_gpu"] == n
+    assert r["value"] > 0 and r["unit"] == "Mpkt/s"
+    # value = frames of all ranks / max-over-ranks time
+    assert abs(r["value"] - 2 * n * 3 / (r["ms_per_step"] * 3 * 1e-3) / 1e6) < 0.02 * r["value"]
+    assert "cpu_baseline" not in r            # rank 0 at N=1 only

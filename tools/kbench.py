@@ -50,6 +50,12 @@ def main():
         l.zp_parse_batch_device.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_uint64] + \
             [ctypes.c_void_p] * 3
         libs[v] = l
+    try:
+        rb = libs.get("base", zp._lib.hip())
+        rb.zp_debug_resident_blocks.restype = ctypes.c_uint64
+        print(f"resident blocks (persistent grid): {rb.zp_debug_resident_blocks()}", flush=True)
+    except AttributeError:
+        pass
     sizes = {"c1": 1 << 20, "c2": 1 << 20, "c3": 1 << 24, "c4": 1 << 24, "c5": 1 << 25}
     if args.membw:
         mb = ctypes.CDLL(os.path.join(ROOT, "tools", "libmembw.so"))

@@ -10,7 +10,7 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-NAMES = ["desc", "issue0", "stream", "walk", "verdict"]
+NAMES = ["desc+setup", "issue0", "stream", "walk+verdict"]
 
 
 def main():
@@ -37,10 +37,10 @@ def main():
             run()
             torch.cuda.synchronize()
             lib.zp_stamps_set(None)
-            t = buf.view(nw, 8).cpu().numpy().astype(np.int64)[:, :6] * 10  # ns
+            t = buf.view(nw, 8).cpu().numpy().astype(np.int64)[:, :len(NAMES) + 1] * 10  # ns
             d = np.diff(t, axis=1)
-            life = t[:, 5] - t[:, 0]
-            kern = t[:, 5].max() - t[:, 0].min()
+            life = t[:, -1] - t[:, 0]
+            kern = t[:, -1].max() - t[:, 0].min()
             # average number of resident waves = sum(lifetimes) / kernel span
             print(f"{variant} {cfg}: kernel span {kern/1e6:.3f} ms, wave life mean "
                   f"{life.mean()/1e3:.1f} us (p50 {np.median(life)/1e3:.1f}, p99 "

@@ -7,23 +7,15 @@
 // icmpv4.rs:92-104, icmpv6.rs:89-101) and the checksum primitives
 // (checksum.rs:5-69).
 //
-// Work decomposition. Every wave is independent and owns 64 consecutive
-// frames (lane j = frame j); a workgroup is 4 waves packed for occupancy and
-// never synchronises. Per wave:
-//   A.  one round trip of cooperative, coalesced loads: for each frame the
-//       16-B aligned chunks [A&~15, +256) — chunks 0-7 are the 128-B header
-//       window (-> LDS), chunks 8-15 the "seam" up to the next 128-B line
-//       boundary (summed in registers). One 16-lane DPP row per frame.
-//   A2. the frame's partial last 128-B line (summed), issued together with
-//       the first stream group so both are in flight during the walk.
-//   B.  lane-per-frame header walk from the LDS window.
-//   C.  stream: the frame's full 128-B lines strictly inside it, wave-wide
-//       coalesced loads, ZP_G items per group, two groups in flight.
-//   D.  checksum verdict, 32-B record store.
-// Line ownership: every line a frame shares with a neighbour or with its own
-// window is read in A/A2 (close in time, so the second reader hits L2); C
-// reads lines that belong to one frame only, each exactly once.
-//
+// Work decomposition. A tile is 64 consecutive frames on one wave (lane j =
+// frame j); waves never synchronise with each other. Per tile:
+//   1. descriptors (offs/lens);
+//   2. the packed stream: every byte of the tile's frames read once by full
+//      1 KiB wave-wide loads (the 16-B chunks of all 64 frames concatenated
+//      and cut into items of 64 chunks; see "The stream" below); per-frame
+//      sums by running prefix; header windows and last chunks to LDS;
+//   3. lane-per-frame header walk from the LDS window;
+//   4. checksum verdict, 32-B record store.
 // Checksum arithmetic. The reference verifies S = acc + sum of big-endian
 // 16-bit words (u32), valid iff !fold(S) as u16 == 0 (checksum.rs:5-35),
 // i.e. S != 0 and S == 0 (mod 65535). We sum little-endian 16-bit words at
@@ -55,9 +47,6 @@
 #endif
 #ifndef ZP_G
 #define ZP_G 8               // stream items (1 KiB loads) per group
-#endif
-#ifndef ZP_G0
-#define ZP_G0 ZP_G           // items of a tile's first group (issued before the previous walk)
 #endif
 // Timing-only ablations (tools/build_variants.sh); never set in the product:
 //   ZP_ABL_FAKE_WALK  replace the walk by "pending L4 at offset 42"
@@ -225,9 +214,24 @@ __device__ __forceinline__ uint32_t rd16(FrameView& f, uint32_t x) {
     return (rd8(f, x) << 8) | rd8(f, x + 1);
 }
 
-// Arena-parity word sum V of frame bytes [lo, hi) (both <= len).
-__device__ uint32_t sumV(FrameView& f, uint32_t lo, uint32_t hi) {
-    uint32_t s = 0;
+// Masked sums of a 16-B chunk's bytes [l, h): V (LE words at even addresses)
+// and B (plain byte sum).
+__device__ __forceinline__ void chunk_vb(uint4 v, int l, int h, uint32_t& V, uint32_t& B) {
+    const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t x = (l == 0 && h == 16) ? d[i] : d[i] & byte_mask(4 * i, l, h);
+        V = sad16(x, V);
+        B = __builtin_amdgcn_sad_u8(x, 0u, B);
+    }
+}
+
+// V and B over frame bytes [lo, hi) (both <= len): window chunks from LDS,
+// chunks past the window through the fallback cache.
+template <bool WANT_B>
+__device__ void sum_vb(FrameView& f, uint32_t lo, uint32_t hi, uint32_t& V, uint32_t& B) {
+    V = 0;
+    B = 0;
     const uint32_t h1 = hi < f.wlen ? hi : f.wlen;
     if (lo < h1) {
         const int ylo = (int)(lo + f.shift), yhi = (int)(h1 + f.shift);
@@ -235,7 +239,8 @@ __device__ uint32_t sumV(FrameView& f, uint32_t lo, uint32_t hi) {
         for (int c = c0; c <= c1; ++c) {
             const int l = c == c0 ? ylo - 16 * c : 0;
             const int h = c == c1 ? yhi - 16 * c : 16;
-            s = chunk_sum(win_chunk(f, c), l, h, s);
+            if (WANT_B) chunk_vb(win_chunk(f, c), l, h, V, B);
+            else V = chunk_sum(win_chunk(f, c), l, h, V);
         }
     }
     const uint32_t l2 = lo > f.wlen ? lo : f.wlen;
@@ -245,10 +250,17 @@ __device__ uint32_t sumV(FrameView& f, uint32_t lo, uint32_t hi) {
         for (int c = c0; c <= c1; ++c) {
             const int l = c == c0 ? ylo - 16 * c : 0;
             const int h = c == c1 ? yhi - 16 * c : 16;
-            s = chunk_sum(fb_chunk(f, (uint32_t)c), l, h, s);
+            if (WANT_B) chunk_vb(fb_chunk(f, (uint32_t)c), l, h, V, B);
+            else V = chunk_sum(fb_chunk(f, (uint32_t)c), l, h, V);
         }
     }
-    return s;
+}
+
+// Arena-parity word sum V of frame bytes [lo, hi).
+__device__ __forceinline__ uint32_t sumV(FrameView& f, uint32_t lo, uint32_t hi) {
+    uint32_t V, B;
+    sum_vb<false>(f, lo, hi, V, B);
+    return V;
 }
 
 // V-sum of the bytes [A & ~15, A) that precede the frame in its first chunk.
@@ -257,8 +269,16 @@ __device__ __forceinline__ uint32_t sum_head(const FrameView& f) {
 }
 
 // Exact big-endian word sum (reference parity: words start at lo) of frame
-// bytes [lo, hi): split into even/odd-offset byte sums.
+// bytes [lo, hi), hi - lo even: with E/O the byte sums at even/odd ARENA
+// addresses, V = E + 256*O and B = E + O, so O = (V - B) / 255 exactly; the
+// words start at an even address iff A + lo is even.
 __device__ uint32_t sumW_exact(FrameView& f, uint32_t lo, uint32_t hi) {
+#ifndef ZP_SUMW_BYTES
+    uint32_t V, B;
+    sum_vb<true>(f, lo, hi, V, B);
+    const uint32_t O = (V - B) / 255u, E = B - O;
+    return (((uintptr_t)f.g + lo) & 1) ? 256u * O + E : 256u * E + O;
+#else   // A/B reference: dword-wise from the window, bytewise past it
     uint32_t E = 0, O = 0;
     for (uint32_t x = lo; x < hi; x += 4) {
         uint32_t v;
@@ -273,11 +293,11 @@ __device__ uint32_t sumW_exact(FrameView& f, uint32_t lo, uint32_t hi) {
             for (int k = 0; k < n; ++k) v |= rd8(f, x + k) << (8 * k);
         }
         v &= byte_mask(0, 0, n);
-        // offsets relative to lo: even ones are the high bytes of the words
         E += (v & 0xFFu) + ((v >> 16) & 0xFFu);
         O += ((v >> 8) & 0xFFu) + (v >> 24);
     }
     return 256u * E + O;
+#endif
 }
 
 // Exact reference checksum for long segments: sums even/odd-address bytes
@@ -395,7 +415,7 @@ __device__ void walk_frame(FrameView& f, Walk& w) {
             bool v4 = et == 0x0800;
             for (uint32_t level = 0;; ++level) {
                 const uint32_t sl = len - pos;                        // slice length
-                uint32_t proto, pp, acc;
+                uint32_t proto, pp;
                 if (v4) {                                             // parser.rs:188-212
                     if (sl < 20) { err = ZP_ERR_IPV4_TOO_SHORT; goto done; }
                     const uint32_t b0 = rd8(f, pos);
@@ -408,8 +428,6 @@ __device__ void walk_frame(FrameView& f, Walk& w) {
                     if (!(hv != 0 && hv % 65535u == 0)) { err = ZP_ERR_IPV4_CHECKSUM; goto done; }
                     proto = rd8(f, pos + 9);
                     pp = pos + ihl;
-                    // parser.rs:322-326: no pseudo-header for ICMPv4
-                    acc = proto == 1 ? 0u : sumW_exact(f, pos + 12, pos + 20) + proto + (len - pp);
                     if (level == 0) r.flags |= ZP_F_IPV4;
                     else if (level == 1) { r.flags |= ZP_F_IP_IN_IP; r.inner_off = pos; }
                 } else {                                              // parser.rs:222-230
@@ -422,7 +440,6 @@ __device__ void walk_frame(FrameView& f, Walk& w) {
                     if ((rd8(f, pos) >> 4) != 6) { err = ZP_ERR_IPV6_VERSION; goto done; }
                     proto = pres ? fin : nh;                          // ipv6.rs:219-227
                     pp = pos + 40 + tot;                              // ipv6.rs:283-285
-                    acc = sumW_exact(f, pos + 8, pos + 40) + proto + (len - pp);  // parser.rs:349-354
                     if (level == 0) {
                         r.flags |= ZP_F_IPV6;
                         r.final_nh = (uint8_t)proto;
@@ -470,9 +487,13 @@ __device__ void walk_frame(FrameView& f, Walk& w) {
                 } else {
                     break;                                            // unknown: Ok, no L4
                 }
+                // Pseudo-header of the innermost IP only (outer levels of an
+                // IP-in-IP chain never need one): parser.rs:316-333 (IPv4;
+                // none for ICMPv4), parser.rs:341-361 (IPv6, final next header).
+                w.acc = v4 ? (proto == 1 ? 0u : sumW_exact(f, pos + 12, pos + 20) + proto + (len - pp))
+                           : sumW_exact(f, pos + 8, pos + 40) + proto + (len - pp);
                 r.l4_off = pp;
                 w.pending = 1;
-                w.acc = acc;
                 w.l4 = pp;
                 w.v6 = v4 ? 0 : 1;
                 break;
@@ -798,14 +819,10 @@ __device__ __forceinline__ void load_desc(const uint8_t* arena, const uint64_t* 
     ga = (uintptr_t)arena + (p < n ? o : 0);
 }
 
-// Persistent grid: wave gw handles tiles gw, gw + W, ... (W = all waves of
-// the grid, sized to the resident capacity by the launcher). Per tile:
-//   descriptors of the next tile      (loads, land during this tile's stream)
-//   stream groups 1..                 (group 0 was issued and consumed before)
-//   setup + issue of the next tile's group 0   } ZP_OVERLAP: the next tile's
-//   walk + verdict of this tile                } first loads fly during the walk
-//   consume of the next tile's group 0
-// No load is in flight across the loop back-edge (see issue_group).
+// One wave per tile; the hardware back-fills finished waves with the next
+// tiles in dispatch order, so the resident waves always stream a contiguous
+// band of the arena (measured: a persistent grid looping over tiles was
+// 9-12 % slower on c3/c5).
 __global__ void __launch_bounds__(64 * ZP_WAVES)
 zp_parse_kernel(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs,
                 const uint32_t* __restrict__ lens, uint64_t n,
@@ -814,80 +831,36 @@ zp_parse_kernel(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ 
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
     WaveLds& lds = lds_all[wid];
-    const uint64_t ntiles = (n + 63) / 64;
-    const uint64_t W = (uint64_t)gridDim.x * ZP_WAVES;
-    uint64_t t = (uint64_t)blockIdx.x * ZP_WAVES + wid;
-    if (t >= ntiles) return;                       // wave-uniform
+    const uint64_t t = (uint64_t)blockIdx.x * ZP_WAVES + wid;
+    if (t * 64 >= n) return;                       // wave-uniform
+#ifdef ZP_STAMPS
+    const uint64_t wave_id = t;
+#endif
+    STAMP(0);
     const uintptr_t fallback = (uintptr_t)&zp_safe_chunk;   // dummy loads when T == 0
     uint4* win = &lds.win[0];
     uint4* tail = &lds.win[ZP_WIN_CH * 64];
-    uint4 va[ZP_G], v0[ZP_G0];
-    uint32_t ka[ZP_G], k0[ZP_G0];
-    TileState s, sn;
-    {
-        uint32_t len;
-        uintptr_t ga;
-        load_desc(arena, offs, lens, n, t, lane, len, ga);
-        tile_setup(s, t, len, ga, n, lane, lds);
-        issue_group<ZP_G0>(0, s.nitems, s.cur, s.R, lane, fallback, v0, k0);
-        wave_lds_fence();
-        consume_group<ZP_G0>(0, s.nitems, lane, v0, k0, win, tail, lds.cend, s.run);
+    uint32_t len;
+    uintptr_t ga;
+    load_desc(arena, offs, lens, n, t, lane, len, ga);
+    TileState s;
+    tile_setup(s, t, len, ga, n, lane, lds);
+    STAMP(1);
+    // stream: one group of ZP_G items per iteration (group 0 outside the loop,
+    // so no load is in flight across the loop back-edge)
+    uint4 va[ZP_G];
+    uint32_t ka[ZP_G];
+    issue_group<ZP_G>(0, s.nitems, s.cur, s.R, lane, fallback, va, ka);
+    STAMP(2);
+    consume_group<ZP_G>(0, s.nitems, lane, va, ka, win, tail, lds.cend, s.run);
+    for (uint32_t i0 = ZP_G; i0 < s.nitems; i0 += ZP_G) {
+        issue_group<ZP_G>(i0, s.nitems, s.cur, s.R, lane, fallback, va, ka);
+        consume_group<ZP_G>(i0, s.nitems, lane, va, ka, win, tail, lds.cend, s.run);
     }
-    for (;;) {
-#ifdef ZP_STAMPS
-        const uint64_t wave_id = t;
-#endif
-        STAMP(0);
-        const uint64_t tn = t + W;
-        const bool more = tn < ntiles;             // wave-uniform
-        uint32_t len_n;
-        uintptr_t ga_n;
-        load_desc(arena, offs, lens, n, more ? tn : t, lane, len_n, ga_n);
-        if (!more) len_n = 0;                      // a dummy tile: no chunks, dummy loads
-        STAMP(1);
-        for (uint32_t i0 = ZP_G0; i0 < s.nitems; i0 += ZP_G) {
-            issue_group<ZP_G>(i0, s.nitems, s.cur, s.R, lane, fallback, va, ka);
-            consume_group<ZP_G>(i0, s.nitems, lane, va, ka, win, tail, lds.cend, s.run);
-        }
-        wave_lds_fence();
-        STAMP(2);
-#ifdef ZP_OVERLAP
-        tile_setup(sn, tn, len_n, ga_n, n, lane, lds);
-        issue_group<ZP_G0>(0, sn.nitems, sn.cur, sn.R, lane, fallback, v0, k0);
-        tile_finish(s, n, lane, lds, records, inner_ext);
-#else
-        tile_finish(s, n, lane, lds, records, inner_ext);
-        tile_setup(sn, tn, len_n, ga_n, n, lane, lds);
-        issue_group<ZP_G0>(0, sn.nitems, sn.cur, sn.R, lane, fallback, v0, k0);
-#endif
-        STAMP(3);
-        wave_lds_fence();
-        consume_group<ZP_G0>(0, sn.nitems, lane, v0, k0, win, tail, lds.cend, sn.run);
-        STAMP(4);
-        if (!more) break;
-        s = sn;
-        t = tn;
-    }
-}
-
-// Workgroups of zp_parse_kernel resident at once on the current device (CUs x
-// occupancy), cached per device. 0 = unknown (launch one wave per tile).
-static uint64_t resident_blocks() {
-    static uint64_t cache[64];
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
-    if (!cache[dev]) {
-        int per_cu = 0, cus = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, zp_parse_kernel, 64 * ZP_WAVES, 0)
-                != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            per_cu <= 0 || cus <= 0) {
-            (void)hipGetLastError();
-            return 0;
-        }
-        cache[dev] = (uint64_t)per_cu * (uint64_t)cus;
-    }
-    return cache[dev];
+    wave_lds_fence();                              // LDS written by other lanes
+    STAMP(3);
+    tile_finish(s, n, lane, lds, records, inner_ext);
+    STAMP(4);
 }
 
 extern "C" int zp_parse_batch_device(const uint8_t* arena, const uint64_t* offs,
@@ -899,9 +872,11 @@ extern "C" int zp_parse_batch_device(const uint8_t* arena, const uint64_t* offs,
         snprintf(g_last_error, sizeof g_last_error, "zp_parse_batch_device: null pointer");
         return -1;
     }
-    uint64_t blocks = (n + 64 * ZP_WAVES - 1) / (64 * ZP_WAVES);
-    const uint64_t cap = resident_blocks();
-    if (cap && blocks > cap) blocks = cap;       // persistent: waves loop over tiles
+    const uint64_t blocks = (n + 64 * ZP_WAVES - 1) / (64 * ZP_WAVES);
+    if (blocks > 0x7FFFFFFFull) {
+        snprintf(g_last_error, sizeof g_last_error, "zp_parse_batch_device: batch too large");
+        return -1;
+    }
     hipLaunchKernelGGL(zp_parse_kernel, dim3((unsigned)blocks), dim3(64 * ZP_WAVES), 0,
                        (hipStream_t)stream, arena, offs, lens, n, records, inner_ext);
     const hipError_t e = hipGetLastError();
