@@ -126,8 +126,8 @@ def pcie_inclusive(zp, arena, offs, lens, sample_pkts):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="c3", choices=sorted(WORKLOADS))
     ap.add_argument("--packets", type=int, default=0, help="frames per GPU (default: config)")
     ap.add_argument("--cpu-sample", type=int, default=1 << 20)

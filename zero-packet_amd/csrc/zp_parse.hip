@@ -664,10 +664,13 @@ __device__ __forceinline__ void consume_group(uint32_t i0, uint32_t nitems, int 
                                               const uint4 (&v)[G], const uint32_t (&keep)[G],
                                               uint4* win, uint4* tail, uint32_t* cend,
                                               uint32_t& run) {
+    // Items past the end (wave-uniform) are skipped by a branch, not a
+    // loop exit: with `break` LLVM stops fully unrolling past G = 8 and the
+    // group arrays go to scratch.
 #pragma unroll
     for (int q = 0; q < G; ++q) {
         const uint32_t i = i0 + q;
-        if (i >= nitems) break;                               // wave-uniform
+        if (i >= nitems) continue;                            // wave-uniform
         const uint32_t k = keep[q];
         if (k & KEEP_WIN) win[k & 0x1FFu] = v[q];
         uint32_t part = sad16(v[q].x, 0u);
