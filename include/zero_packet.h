@@ -191,6 +191,105 @@ int zp_parse_one(zp_ctx* ctx, const uint8_t* frame, uint64_t len,
                  zp_record* record, zp_ext_offsets* inner_ext);
 
 /* ------------------------------------------------------------------------- */
+/* Host-ring ingestion pipeline. Frames start in host */
+/* memory (a NIC ring / raw socket, README.md:85-115 of the reference). A     */
+/* ring holds `nslots` slots, each with pinned host buffers, device buffers   */
+/* and its own stream. The producer acquires a slot, fills its arena and      */
+/* descriptors in place (a NIC would DMA straight into the pinned arena) and  */
+/* submits it; the slot then runs H2D -> parse -> D2H asynchronously while    */
+/* the next slot fills. The consumer takes completed slots in submission      */
+/* order (wait / poll), reads the records and releases the slot.              */
+/* Slot states: FREE -acquire-> FILLING -submit-> IN_FLIGHT -wait/poll->      */
+/* DONE -release-> FREE. One producer and one consumer thread may use a ring  */
+/* concurrently. All functions return 0 on success, negative on error (see    */
+/* zp_last_error()), ZP_RING_TIMEOUT when a wait expires.                     */
+/* ------------------------------------------------------------------------- */
+typedef struct zp_ring zp_ring;
+#define ZP_RING_TIMEOUT (-4)
+typedef struct zp_ring_slot {
+    int32_t id;                         /* slot index                          */
+    uint8_t* arena;                     /* pinned host arena, arena_cap bytes  */
+    uint64_t* offs;                     /* pinned frame offsets into arena     */
+    uint32_t* lens;                     /* pinned frame lengths                */
+    uint64_t arena_cap, frames_cap;
+    const zp_record* records;           /* results (valid after wait/poll)     */
+    const zp_ext_offsets* inner_ext;    /* written where ZP_F_INNER_EXT is set */
+    uint64_t n;                         /* frames in the slot (after wait/poll) */
+    uint64_t seq;                       /* submission sequence number          */
+} zp_ring_slot;
+
+zp_ring* zp_ring_create(int device, uint32_t nslots, uint64_t slot_bytes,
+                        uint64_t slot_frames);
+void zp_ring_destroy(zp_ring* ring);
+/* Hands out the next slot (in ring order) once it is FREE, as FILLING.
+ * timeout_ms < 0 blocks, 0 only checks; ZP_RING_TIMEOUT when it expires. */
+int zp_ring_acquire(zp_ring* ring, zp_ring_slot* slot, int64_t timeout_ms);
+/* Enqueues H2D + parse + D2H for the first n frames of an acquired slot.
+ * Frames must lie inside the slot arena (else -1, nothing enqueued). */
+int zp_ring_submit(zp_ring* ring, int32_t id, uint64_t n);
+/* Hands out the oldest submitted slot once its records are in host memory.
+ * timeout_ms < 0 blocks, 0 polls; ZP_RING_TIMEOUT when nothing is ready. */
+int zp_ring_wait(zp_ring* ring, zp_ring_slot* slot, int64_t timeout_ms);
+/* Returns a DONE slot to the producer. */
+int zp_ring_release(zp_ring* ring, int32_t id);
+
+/* ------------------------------------------------------------------------- */
+/* Column views: the reader getters of every parsed  */
+/* frame gathered into SoA device columns, so downstream consumers get ready */
+/* columns (5-tuple, VLAN TCIs, flow label ...) without a host pass.         */
+/* Entry i of a column is 0 when record i holds an error or the reader the   */
+/* column belongs to is absent. Multi-byte integers are host order (LE);     */
+/* byte-array columns (MACs, addresses) are the frame bytes as they stand.   */
+/* "outer IP" = PacketParser::ipv4 / ::ipv6, "inner IP" = ::ip_in_ip.        */
+/* ------------------------------------------------------------------------- */
+typedef enum zp_col {
+    ZP_COL_DEST_MAC = 0,     /* u8[6]  EthernetReader::dest_mac (ethernet.rs:195-198)     */
+    ZP_COL_SRC_MAC,          /* u8[6]  EthernetReader::src_mac (ethernet.rs:201-204)      */
+    ZP_COL_ETHERTYPE,        /* u16    EthernetReader::ethertype (ethernet.rs:209-212)    */
+    ZP_COL_VLAN_TCI,         /* u16    vlan_tag().1, or double_vlan_tag().0.1 (:218-244)  */
+    ZP_COL_VLAN_INNER_TCI,   /* u16    double_vlan_tag().1.1 (ethernet.rs:232-244)        */
+    ZP_COL_ARP_OPER,         /* u16    ArpReader::oper (arp.rs:174-177)                   */
+    ZP_COL_IP_VERSION,       /* u8     4 or 6 when the outer IP reader is present         */
+    ZP_COL_SRC_ADDR,         /* u8[16] IPv4Reader::src_ip in bytes 0-3 (ipv4.rs:210-213)  */
+                             /*        or IPv6Reader::src_addr (ipv6.rs:245-248)          */
+    ZP_COL_DEST_ADDR,        /* u8[16] dest_ip (ipv4.rs:216-219) / dest_addr (ipv6.rs:253-256) */
+    ZP_COL_PROTOCOL,         /* u8     IPv4 protocol (ipv4.rs:204-207) / IPv6             */
+                             /*        final_next_header (ipv6.rs:219-227)                */
+    ZP_COL_TTL,              /* u8     ttl (ipv4.rs:198-201) / hop_limit (ipv6.rs:237-240) */
+    ZP_COL_TOS,              /* u8     dscp<<2|ecn (ipv4.rs:160-169) / traffic_class (ipv6.rs:181) */
+    ZP_COL_IP_ID,            /* u32    IPv4 id (ipv4.rs:180) / flow_label (ipv6.rs:189)    */
+    ZP_COL_IP_LEN,           /* u16    total_length (ipv4.rs:174) / payload_length (ipv6.rs:199)*/
+    ZP_COL_INNER_VERSION,    /* u8     4 or 6 when ip_in_ip is present (misc.rs:6-9)      */
+    ZP_COL_INNER_SRC_ADDR,   /* u8[16] as ZP_COL_SRC_ADDR, of the ip_in_ip reader         */
+    ZP_COL_INNER_DEST_ADDR,  /* u8[16]                                                    */
+    ZP_COL_INNER_PROTOCOL,   /* u8     protocol / final_next_header of ip_in_ip           */
+    ZP_COL_L4_PROTO,         /* u8     6 tcp, 17 udp, 1 icmpv4, 58 icmpv6; 0 none         */
+    ZP_COL_SRC_PORT,         /* u16    TcpReader / UdpReader::src_port (tcp.rs:151, udp.rs:113) */
+    ZP_COL_DEST_PORT,        /* u16    dest_port (tcp.rs:157, udp.rs:119)                 */
+    ZP_COL_TCP_SEQ,          /* u32    sequence_number (tcp.rs:163-170)                   */
+    ZP_COL_TCP_ACK,          /* u32    ack_number (tcp.rs:172-179)                        */
+    ZP_COL_TCP_FLAGS,        /* u8     flags (tcp.rs:193-196)                             */
+    ZP_COL_TCP_WINDOW,       /* u16    window_size (tcp.rs:199-202)                       */
+    ZP_COL_ICMP_TYPE,        /* u8     icmp_type (icmpv4.rs:102, icmpv6.rs:99)            */
+    ZP_COL_ICMP_CODE,        /* u8     icmp_code (icmpv4.rs:108, icmpv6.rs:105)           */
+    ZP_COL_L4_CHECKSUM,      /* u16    checksum() (tcp.rs:205, udp.rs:125, icmpv4.rs:114) */
+    ZP_COL_PAYLOAD_OFF,      /* u32    frame offset of the L4 reader's payload(); 0 when  */
+                             /*        absent or when payload() returns Err (tcp.rs:235-243) */
+    ZP_COL_COUNT
+} zp_col;
+
+/* Element size in bytes of column `col` (0 if out of range). */
+int zp_col_width(int col);
+
+/* Fills the requested columns for n parsed frames: cols[c] is a device array
+ * of n * zp_col_width(c) bytes, or NULL to skip column c. arena/offs/lens are
+ * the batch given to zp_parse_batch_device, records its output (device
+ * memory). Enqueues on `stream`; returns 0 or negative on launch failure. */
+int zp_extract_columns_device(const uint8_t* arena, const uint64_t* offs,
+                              const uint32_t* lens, const zp_record* records, uint64_t n,
+                              void* const* cols, void* stream);
+
+/* ------------------------------------------------------------------------- */
 /* Synthetic batch generator (BASELINE.json configs 1-5), built from the      */
 /* builder's checksum-fill semantics (builder.rs:473-474,515-516,553,592-593).*/
 /* Deterministic per packet: packet i depends only on (config, seed, i).      */

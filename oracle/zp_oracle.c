@@ -444,3 +444,119 @@ int zpo_parse_batch(const uint8_t* arena, const uint64_t* offs, const uint32_t* 
     for (int t = 0; t < nthreads; ++t) if (started[t]) pthread_join(th[t], 0);
     return nthreads;
 }
+
+/* ---- column views -------------------------------- */
+/* The reader getters restated over the frame bytes at the record's offsets:
+ * EthernetReader (ethernet.rs:195-244), ArpReader::oper (arp.rs:174-177),
+ * IPv4Reader (ipv4.rs:148-227), IPv6Reader (ipv6.rs:173-256), TcpReader
+ * (tcp.rs:151-243), UdpReader (udp.rs:113-154), Icmpv4/6Reader
+ * (icmpv4.rs:102-135, icmpv6.rs:99-132). The record says which readers the
+ * parser holds (parser.rs:22-32); include/zero_packet.h defines each column. */
+
+static const int col_width[ZP_COL_COUNT] = {
+    6, 6, 2, 2, 2, 2, 1, 16, 16, 1, 1, 1, 4, 2, 1, 16, 16, 1, 1, 2, 2, 4, 4, 1, 2, 1, 1, 2, 4};
+
+static void put(void* const* cols, int c, uint64_t i, const void* v) {
+    if (cols[c]) memcpy((uint8_t*)cols[c] + i * (uint64_t)col_width[c], v, (size_t)col_width[c]);
+}
+static void put8(void* const* cols, int c, uint64_t i, uint8_t v) { put(cols, c, i, &v); }
+static void put16(void* const* cols, int c, uint64_t i, uint16_t v) { put(cols, c, i, &v); }
+static void put32(void* const* cols, int c, uint64_t i, uint32_t v) { put(cols, c, i, &v); }
+static uint32_t be32(slice_t s, size_t i) {
+    return ((uint32_t)s.p[i] << 24) | ((uint32_t)s.p[i + 1] << 16) | ((uint32_t)s.p[i + 2] << 8) |
+           s.p[i + 3];
+}
+
+/* One IP reader (outer: c0 = ZP_COL_IP_VERSION, inner: ZP_COL_INNER_VERSION). */
+static void ip_columns(void* const* cols, uint64_t i, slice_t ip, int v6, uint8_t final_nh,
+                       int inner) {
+    uint8_t src[16] = {0}, dst[16] = {0};
+    const int cv = inner ? ZP_COL_INNER_VERSION : ZP_COL_IP_VERSION;
+    const int cs = inner ? ZP_COL_INNER_SRC_ADDR : ZP_COL_SRC_ADDR;
+    const int cd = inner ? ZP_COL_INNER_DEST_ADDR : ZP_COL_DEST_ADDR;
+    const int cp = inner ? ZP_COL_INNER_PROTOCOL : ZP_COL_PROTOCOL;
+    if (!v6) {
+        put8(cols, cv, i, (uint8_t)(ip.p[0] >> 4));               /* ipv4.rs:148-151 */
+        memcpy(src, ip.p + 12, 4);                                 /* ipv4.rs:210-213 */
+        memcpy(dst, ip.p + 16, 4);                                 /* ipv4.rs:216-219 */
+        put8(cols, cp, i, ip.p[9]);                                /* ipv4.rs:204-207 */
+    } else {
+        put8(cols, cv, i, (uint8_t)(ip.p[0] >> 4));               /* ipv6.rs:173-176 */
+        memcpy(src, ip.p + 8, 16);                                 /* ipv6.rs:245-248 */
+        memcpy(dst, ip.p + 24, 16);                                /* ipv6.rs:253-256 */
+        put8(cols, cp, i, final_nh);                               /* ipv6.rs:219-227 */
+    }
+    put(cols, cs, i, src);
+    put(cols, cd, i, dst);
+    if (inner) return;
+    if (!v6) {
+        put8(cols, ZP_COL_TTL, i, ip.p[8]);                        /* ipv4.rs:198-201 */
+        put8(cols, ZP_COL_TOS, i, ip.p[1]);                        /* dscp<<2|ecn :160-169 */
+        put32(cols, ZP_COL_IP_ID, i, be16(ip, 4));                 /* ipv4.rs:180-183 */
+        put16(cols, ZP_COL_IP_LEN, i, be16(ip, 2));                /* ipv4.rs:174-177 */
+    } else {
+        put8(cols, ZP_COL_TTL, i, ip.p[7]);                        /* ipv6.rs:237-240 */
+        put8(cols, ZP_COL_TOS, i,                                  /* ipv6.rs:181-186 */
+             (uint8_t)(((ip.p[0] & 0x0F) << 4) | (ip.p[1] >> 4)));
+        put32(cols, ZP_COL_IP_ID, i,                               /* ipv6.rs:189-196 */
+              ((uint32_t)(ip.p[1] & 0x0F) << 16) | ((uint32_t)ip.p[2] << 8) | ip.p[3]);
+        put16(cols, ZP_COL_IP_LEN, i, be16(ip, 4));                /* ipv6.rs:199-202 */
+    }
+}
+
+int zpo_columns(const uint8_t* arena, const uint64_t* offs, const uint32_t* lens,
+                const zp_record* recs, uint64_t n, void* const* cols) {
+    for (int c = 0; c < ZP_COL_COUNT; ++c)
+        if (cols[c]) memset(cols[c], 0, n * (uint64_t)col_width[c]);
+    for (uint64_t i = 0; i < n; ++i) {
+        const zp_record* r = &recs[i];
+        if (r->err || !(r->flags & ZP_F_ETHERNET)) continue;
+        slice_t fr = {arena + offs[i], lens[i]};
+        const uint32_t hl = r->eth_len;
+        put(cols, ZP_COL_DEST_MAC, i, fr.p);                       /* ethernet.rs:195-198 */
+        put(cols, ZP_COL_SRC_MAC, i, fr.p + 6);                    /* ethernet.rs:201-204 */
+        put16(cols, ZP_COL_ETHERTYPE, i, be16(fr, hl - 2));        /* ethernet.rs:209-212 */
+        if (be16(fr, 12) == 0x8100) {                              /* vlan_tag :218-229 */
+            put16(cols, ZP_COL_VLAN_TCI, i, be16(fr, 14));
+        } else if (be16(fr, 12) == 0x88A8) {                       /* double_vlan_tag :232-244 */
+            put16(cols, ZP_COL_VLAN_TCI, i, be16(fr, 14));
+            put16(cols, ZP_COL_VLAN_INNER_TCI, i, be16(fr, 18));
+        }
+        if (r->flags & ZP_F_ARP) put16(cols, ZP_COL_ARP_OPER, i, be16(sub(fr, hl), 6));
+        if (r->flags & (ZP_F_IPV4 | ZP_F_IPV6))
+            ip_columns(cols, i, sub(fr, hl), (r->flags & ZP_F_IPV6) != 0, r->final_nh, 0);
+        if (r->flags & ZP_F_IP_IN_IP)
+            ip_columns(cols, i, sub(fr, r->inner_off), (r->flags & ZP_F_IP_IN_IP_V6) != 0,
+                       r->inner_final_nh, 1);
+        const uint32_t l4f = r->flags & (ZP_F_TCP | ZP_F_UDP | ZP_F_ICMPV4 | ZP_F_ICMPV6);
+        if (!l4f) continue;
+        slice_t l4 = sub(fr, r->l4_off);
+        uint32_t hlen;
+        if (l4f == ZP_F_TCP) {
+            put8(cols, ZP_COL_L4_PROTO, i, 6);
+            put16(cols, ZP_COL_SRC_PORT, i, be16(l4, 0));          /* tcp.rs:151-154 */
+            put16(cols, ZP_COL_DEST_PORT, i, be16(l4, 2));         /* tcp.rs:157-160 */
+            put32(cols, ZP_COL_TCP_SEQ, i, be32(l4, 4));           /* tcp.rs:163-170 */
+            put32(cols, ZP_COL_TCP_ACK, i, be32(l4, 8));           /* tcp.rs:172-179 */
+            put8(cols, ZP_COL_TCP_FLAGS, i, l4.p[13]);             /* tcp.rs:193-196 */
+            put16(cols, ZP_COL_TCP_WINDOW, i, be16(l4, 14));       /* tcp.rs:199-202 */
+            put16(cols, ZP_COL_L4_CHECKSUM, i, be16(l4, 16));      /* tcp.rs:205-208 */
+            hlen = (uint32_t)(l4.p[12] >> 4) * 4;                  /* tcp.rs:217-220 */
+        } else if (l4f == ZP_F_UDP) {
+            put8(cols, ZP_COL_L4_PROTO, i, 17);
+            put16(cols, ZP_COL_SRC_PORT, i, be16(l4, 0));          /* udp.rs:113-116 */
+            put16(cols, ZP_COL_DEST_PORT, i, be16(l4, 2));         /* udp.rs:119-122 */
+            put16(cols, ZP_COL_L4_CHECKSUM, i, be16(l4, 6));       /* udp.rs:125-128 */
+            hlen = 8;                                              /* udp.rs:139-142 */
+        } else {
+            put8(cols, ZP_COL_L4_PROTO, i, l4f == ZP_F_ICMPV4 ? 1 : 58);
+            put8(cols, ZP_COL_ICMP_TYPE, i, l4.p[0]);              /* icmpv4.rs:102-105 */
+            put8(cols, ZP_COL_ICMP_CODE, i, l4.p[1]);              /* icmpv4.rs:108-111 */
+            put16(cols, ZP_COL_L4_CHECKSUM, i, be16(l4, 2));       /* icmpv4.rs:114-117 */
+            hlen = 8;                                              /* icmpv4.rs:120-123 */
+        }
+        if (hlen <= l4.n)                                          /* tcp.rs:235-243 */
+            put32(cols, ZP_COL_PAYLOAD_OFF, i, r->l4_off + hlen);
+    }
+    return 0;
+}

@@ -74,3 +74,39 @@ def pseudo_header(src, dst, protocol, length):
     d = ctypes.create_string_buffer(bytes(dst))
     return lib().zpo_pseudo_header(ctypes.addressof(s), ctypes.addressof(d), len(src),
                                    protocol, length)
+
+
+# zp_col order and element layout (include/zero_packet.h), numpy side.
+COLUMN_SPEC = [
+    ("dest_mac", np.uint8, 6), ("src_mac", np.uint8, 6), ("ethertype", np.uint16, 1),
+    ("vlan_tci", np.uint16, 1), ("vlan_inner_tci", np.uint16, 1), ("arp_oper", np.uint16, 1),
+    ("ip_version", np.uint8, 1), ("src_addr", np.uint8, 16), ("dest_addr", np.uint8, 16),
+    ("protocol", np.uint8, 1), ("ttl", np.uint8, 1), ("tos", np.uint8, 1),
+    ("ip_id", np.uint32, 1), ("ip_len", np.uint16, 1), ("inner_version", np.uint8, 1),
+    ("inner_src_addr", np.uint8, 16), ("inner_dest_addr", np.uint8, 16),
+    ("inner_protocol", np.uint8, 1), ("l4_proto", np.uint8, 1), ("src_port", np.uint16, 1),
+    ("dest_port", np.uint16, 1), ("tcp_seq", np.uint32, 1), ("tcp_ack", np.uint32, 1),
+    ("tcp_flags", np.uint8, 1), ("tcp_window", np.uint16, 1), ("icmp_type", np.uint8, 1),
+    ("icmp_code", np.uint8, 1), ("l4_checksum", np.uint16, 1), ("payload_off", np.uint32, 1),
+]
+
+
+def columns(arena, offs, lens, recs):
+    """zpo_columns: the reader getters restated in C -> {name: numpy array}."""
+    arena = np.ascontiguousarray(arena, dtype=np.uint8)
+    offs = np.ascontiguousarray(offs).astype(np.uint64, copy=False)
+    lens = np.ascontiguousarray(lens).astype(np.uint32, copy=False)
+    recs = np.ascontiguousarray(recs)
+    n = len(offs)
+    out = {}
+    ptrs = (ctypes.c_void_p * len(COLUMN_SPEC))()
+    for k, (name, dt, w) in enumerate(COLUMN_SPEC):
+        out[name] = np.zeros((n, w) if w > 1 else (n,), dt)
+        ptrs[k] = out[name].ctypes.data
+    l = lib()
+    l.zpo_columns.restype = ctypes.c_int
+    l.zpo_columns.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_uint64, ctypes.c_void_p]
+    if n:
+        l.zpo_columns(arena.ctypes.data, offs.ctypes.data, lens.ctypes.data, recs.ctypes.data,
+                      n, ptrs)
+    return out

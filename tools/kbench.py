@@ -39,6 +39,7 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--membw", action="store_true")
     ap.add_argument("--no-base", action="store_true", help="time only --variants (PMC runs)")
+    ap.add_argument("--columns", action="store_true", help="also time zp_extract_columns_device")
     args = ap.parse_args()
     zp = importlib.import_module("zero-packet_amd")
     dev = torch.device("cuda:0")
@@ -105,6 +106,22 @@ def main():
             med = float(np.median(ms))
             print(f"{cfg} {name:>12}: {med:8.3f} ms  {nbytes / med / 1e6:7.0f} GB/s  "
                   f"{n / med / 1e3:8.0f} Mpkt/s  (min {min(ms):.3f})", flush=True)
+        if args.columns:
+            zp.batch.parse_batch(arena, offs, lens, rec, ext)
+            for label, names in (("all", zp.columns.NAMES),
+                                 ("5tuple", ["src_addr", "dest_addr", "protocol", "src_port",
+                                             "dest_port"])):
+                out = zp.columns.extract(arena, offs, lens, rec, names=names)
+                ms = time_launches(lambda: zp.columns.extract(arena, offs, lens, rec, names=names,
+                                                              out=out), args.reps * args.rounds)
+                med = float(np.median(ms))
+                wbytes = n * sum(zp.columns.width(c) for c in names)
+                # records + descriptors + one staged 128-B header window per frame
+                rbytes = n * (32 + 12 + 128)
+                print(f"{cfg} columns[{label}]: {med:8.3f} ms  write {wbytes / med / 1e6:6.0f} GB/s"
+                      f"  (write+read {(wbytes + rbytes) / med / 1e6:6.0f} GB/s)  "
+                      f"{n / med / 1e3:8.0f} Mpkt/s", flush=True)
+                del out
         del arena, offs, lens, rec, ext
         torch.cuda.empty_cache()
 

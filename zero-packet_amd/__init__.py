@@ -5,18 +5,20 @@ Import with importlib (the directory name has a hyphen):
 
   zp.batch.parse_batch(arena, offs, lens)   device-resident batch parse (HIP)
   zp.batch.generate(cfg, n)                  synthetic BASELINE configs on the GPU
+  zp.columns.extract(arena, offs, lens, recs) reader getters as SoA device columns
+  zp.ring.Ring(device, slots, slot_bytes)    host-ring ingestion (H2D/parse/D2H in flight)
   zp.PacketParser.parse(frame)               one frame through the GPU path
   zp.PacketParser.from_record(frame, rec)    reference-shaped views over a record
 """
-from . import _lib, records, shard  # noqa: F401
+from . import _lib, records, ring, shard  # noqa: F401
 from .parser import (ArpReader, AuthenticationHeaderReader, EthernetReader,  # noqa: F401
                      ExtensionHeaders, FragmentHeaderReader, Icmpv4Reader, Icmpv6Reader,
                      IpInIp, IPv4Reader, IPv6Reader, OptionsHeaderReader, PacketParser,
                      RoutingHeaderReader, TcpReader, UdpReader, ZeroPacketError)
 
 try:  # torch-dependent batch API
-    from . import batch  # noqa: F401
+    from . import batch, columns  # noqa: F401
 except ImportError:  # pragma: no cover
-    batch = None
+    batch = columns = None
 
 __all__ = ["PacketParser", "ZeroPacketError", "batch", "records"]

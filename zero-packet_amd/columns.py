@@ -1,0 +1,71 @@
+"""Column views over parsed frames (zp_extract_columns_device).
+
+    cols = columns.extract(arena, offs, lens, records, names=("src_port", ...))
+
+Each column is a device tensor of n entries (byte-array columns: [n, width]
+uint8): the reader getters of every frame gathered into SoA form, so a
+downstream consumer (flow table, filter, sampler) needs no host pass. Column
+semantics and the reference getters they follow: include/zero_packet.h
+(zp_col). Entry i is 0 when record i holds an error or the reader is absent.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+
+# (name, torch dtype, elements per frame) in zp_col order.
+COLUMNS = [
+    ("dest_mac", torch.uint8, 6), ("src_mac", torch.uint8, 6),
+    ("ethertype", torch.uint16, 1), ("vlan_tci", torch.uint16, 1),
+    ("vlan_inner_tci", torch.uint16, 1), ("arp_oper", torch.uint16, 1),
+    ("ip_version", torch.uint8, 1), ("src_addr", torch.uint8, 16),
+    ("dest_addr", torch.uint8, 16), ("protocol", torch.uint8, 1), ("ttl", torch.uint8, 1),
+    ("tos", torch.uint8, 1), ("ip_id", torch.uint32, 1), ("ip_len", torch.uint16, 1),
+    ("inner_version", torch.uint8, 1), ("inner_src_addr", torch.uint8, 16),
+    ("inner_dest_addr", torch.uint8, 16), ("inner_protocol", torch.uint8, 1),
+    ("l4_proto", torch.uint8, 1), ("src_port", torch.uint16, 1), ("dest_port", torch.uint16, 1),
+    ("tcp_seq", torch.uint32, 1), ("tcp_ack", torch.uint32, 1), ("tcp_flags", torch.uint8, 1),
+    ("tcp_window", torch.uint16, 1), ("icmp_type", torch.uint8, 1),
+    ("icmp_code", torch.uint8, 1), ("l4_checksum", torch.uint16, 1),
+    ("payload_off", torch.uint32, 1),
+]
+NAMES = [c[0] for c in COLUMNS]
+INDEX = {name: k for k, name in enumerate(NAMES)}
+NUMPY_DTYPE = {torch.uint8: np.uint8, torch.uint16: np.uint16, torch.uint32: np.uint32}
+
+
+def width(name):
+    _, dt, k = COLUMNS[INDEX[name]]
+    return k * torch.empty((), dtype=dt).element_size()
+
+
+def _alloc(name, n, device):
+    _, dt, k = COLUMNS[INDEX[name]]
+    return torch.empty((n, k) if k > 1 else (n,), dtype=dt, device=device)
+
+
+def extract(arena, offs, lens, records, names=None, out=None, stream=None):
+    """Fills the requested columns (default: all) on the device; returns
+    {name: tensor}. `out` may hold preallocated tensors."""
+    for t in (arena, offs, lens, records):
+        if not t.is_cuda:
+            raise RuntimeError("columns.extract needs device tensors (no CPU fallback)")
+    n = offs.numel()
+    assert lens.numel() == n and records.shape[0] == n
+    names = list(names) if names is not None else NAMES
+    out = dict(out or {})
+    ptrs = (ctypes.c_void_p * len(COLUMNS))()
+    for name in names:
+        if name not in out:
+            out[name] = _alloc(name, n, arena.device)
+        t = out[name]
+        assert t.is_contiguous() and t.numel() * t.element_size() == n * width(name), name
+        ptrs[INDEX[name]] = t.data_ptr()
+    s = ctypes.c_void_p(stream) if stream is not None else \
+        ctypes.c_void_p(torch.cuda.current_stream(arena.device).cuda_stream)
+    rc = _lib.hip().zp_extract_columns_device(arena.data_ptr(), offs.data_ptr(), lens.data_ptr(),
+                                              records.data_ptr(), n, ptrs, s)
+    _lib.check(rc, "zp_extract_columns_device")
+    return {k: out[k] for k in names}

@@ -826,7 +826,12 @@ __device__ __forceinline__ void load_desc(const uint8_t* arena, const uint64_t* 
 // tiles in dispatch order, so the resident waves always stream a contiguous
 // band of the arena (measured: a persistent grid looping over tiles was
 // 9-12 % slower on c3/c5).
-__global__ void __launch_bounds__(64 * ZP_WAVES)
+#ifdef ZP_WPE
+#define ZP_KATTR __launch_bounds__(64 * ZP_WAVES) __attribute__((amdgpu_waves_per_eu(ZP_WPE)))
+#else
+#define ZP_KATTR __launch_bounds__(64 * ZP_WAVES)
+#endif
+__global__ void ZP_KATTR
 zp_parse_kernel(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs,
                 const uint32_t* __restrict__ lens, uint64_t n,
                 zp_record* __restrict__ records, zp_ext_offsets* __restrict__ inner_ext) {
