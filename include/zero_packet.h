@@ -290,6 +290,126 @@ int zp_extract_columns_device(const uint8_t* arena, const uint64_t* offs,
                               void* const* cols, void* stream);
 
 /* ------------------------------------------------------------------------- */
+/* Batched PacketBuilder. The reference builds one    */
+/* frame with a typestate chain over a caller-sized buffer                    */
+/* (builder.rs:55-909): PacketBuilder::new(&mut buf).ethernet(..).ipv4(..)    */
+/* .tcp(..).build(). Here every frame of a batch carries its chain as a run   */
+/* of zp_build_op (one op per builder method, in call order) and the kernel   */
+/* executes all chains in place over the frames' buffers, with the writers'   */
+/* exact byte semantics: read-modify-write of shared bytes, checksums over    */
+/* the whole remaining buffer, and the first Err stopping the chain with the  */
+/* partial writes left in place, as the reference leaves them.                */
+/* A chain that the typestate graph (builder.rs:817-909) would not compile    */
+/* is refused before anything is written (ZP_BERR_TRANSITION); a chain whose  */
+/* reference run would panic reports ZP_BERR_PANIC.                           */
+/* ------------------------------------------------------------------------- */
+typedef enum zp_build_kind {
+    ZP_B_ETHERNET = 1,       /* builder.rs:113  src=src_mac dst=dest_mac h0=ethertype      */
+    ZP_B_ETHERNET_VLAN = 2,  /* builder.rs:141  + h1=tci                                    */
+    ZP_B_ETHERNET_QINQ = 3,  /* builder.rs:171  + h1=tci1 h2=tci2                           */
+    ZP_B_ARP = 4,            /* builder.rs:203  h0=htype h1=ptype b0=hlen b1=plen h2=oper   */
+                             /*   src[0:6]=sha src[6:10]=spa dst[0:6]=tha dst[6:10]=tpa      */
+    ZP_B_IPV4 = 5,           /* builder.rs:248/343 b0=version b1=ihl b2=dscp b3=ecn          */
+                             /*   h0=total_length h1=identification b4=flags h2=fragment_offset */
+                             /*   b5=ttl b6=protocol src[0:4]=src_ip dst[0:4]=dest_ip          */
+    ZP_B_IPV6 = 6,           /* builder.rs:300/395 b0=version b1=traffic_class w0=flow_label */
+                             /*   h0=payload_length b2=next_header b3=hop_limit src dst      */
+    ZP_B_HOP_BY_HOP = 7,     /* builder.rs:611  b0=next_header b1=extension_len data=options */
+    ZP_B_DEST_OPTS1 = 8,     /* builder.rs:643  as hop_by_hop                               */
+    ZP_B_ROUTING = 9,        /* builder.rs:675  b0=next_header b1=header_ext_len            */
+                             /*   b2=routing_type b3=segments_left data=data                 */
+    ZP_B_FRAGMENT = 10,      /* builder.rs:711  b0=next_header h0=fragment_offset b1=m_flag */
+                             /*   w0=identification                                          */
+    ZP_B_AUTH = 11,          /* builder.rs:747  b0=next_header b1=payload_len w0=spi        */
+                             /*   w1=seq_num data=auth_data                                  */
+    ZP_B_DEST_OPTS2 = 12,    /* builder.rs:785  as hop_by_hop                               */
+    ZP_B_TCP = 13,           /* builder.rs:438  src/dst = pseudo-header addresses (4 B      */
+                             /*   under IPv4 states, 16 B otherwise) h0=src_port h1=dest_port */
+                             /*   w0=sequence_number w1=acknowledgment_number b0=data_offset  */
+                             /*   b1=reserved b2=flags h2=window_size h3=urgent_pointer      */
+                             /*   data=payload (optional)                                    */
+    ZP_B_UDP = 14,           /* builder.rs:492  src/dst h0=src_port h1=dest_port h2=length  */
+                             /*   data=payload (optional)                                    */
+    ZP_B_ICMPV4 = 15,        /* builder.rs:534  b0=icmp_type b1=icmp_code data=payload (opt) */
+    ZP_B_ICMPV6 = 16,        /* builder.rs:571  src/dst b0=icmp_type b1=icmp_code data (opt) */
+    ZP_B_KIND_COUNT = 17
+} zp_build_kind;
+
+#define ZP_BUILD_NO_DATA 0xFFFFFFFFu   /* data_len: payload None (others: empty)   */
+
+typedef struct zp_build_op {           /* 64 bytes */
+    uint8_t  kind;                     /* zp_build_kind                            */
+    uint8_t  b[7];
+    uint16_t h[4];
+    uint32_t w[2];
+    uint32_t data_off;                 /* variable bytes at data + data_off        */
+    uint32_t data_len;                 /* ... their length, or ZP_BUILD_NO_DATA    */
+    uint8_t  src[16];
+    uint8_t  dst[16];
+} zp_build_op;
+
+typedef enum zp_build_err {
+    ZP_BUILD_OK = 0,
+    ZP_BERR_ETH_SLICE = 1,            /* ethernet.rs:30                            */
+    ZP_BERR_ETH_VLAN = 2,             /* ethernet.rs:85                            */
+    ZP_BERR_ETH_QINQ = 3,             /* ethernet.rs:112                           */
+    ZP_BERR_ARP_DATA = 4,             /* builder.rs:216                            */
+    ZP_BERR_ARP_SLICE = 5,            /* arp.rs:17                                 */
+    ZP_BERR_IPV4_DATA = 6,            /* builder.rs:264,359                        */
+    ZP_BERR_IPV4_SLICE = 7,           /* ipv4.rs:18                                */
+    ZP_BERR_IPV6_DATA = 8,            /* builder.rs:312,407                        */
+    ZP_BERR_IPV6_SLICE = 9,           /* ipv6.rs:18                                */
+    ZP_BERR_TCP_DATA = 10,            /* builder.rs:454                            */
+    ZP_BERR_TCP_SLICE = 11,           /* tcp.rs:17                                 */
+    ZP_BERR_TCP_PAYLOAD = 12,         /* tcp.rs:110 == udp.rs:84                   */
+    ZP_BERR_UDP_DATA = 13,            /* builder.rs:502                            */
+    ZP_BERR_UDP_SLICE = 14,           /* udp.rs:17                                 */
+    ZP_BERR_ICMPV4_DATA = 15,         /* builder.rs:541                            */
+    ZP_BERR_ICMP_SLICE = 16,          /* icmpv4.rs:20 == icmpv6.rs:17              */
+    ZP_BERR_ICMPV4_PAYLOAD = 17,      /* icmpv4.rs:61                              */
+    ZP_BERR_ICMPV6_DATA = 18,         /* builder.rs:580                            */
+    ZP_BERR_ICMPV6_PAYLOAD = 19,      /* icmpv6.rs:58                              */
+    ZP_BERR_HBH_DATA = 20,            /* builder.rs:618                            */
+    ZP_BERR_DEST_DATA = 21,           /* builder.rs:650,792                        */
+    ZP_BERR_OPTIONS_SLICE = 22,       /* options.rs:18                             */
+    ZP_BERR_OPTIONS_MIN = 23,         /* options.rs:54                             */
+    ZP_BERR_OPTIONS_MATCH = 24,       /* options.rs:60                             */
+    ZP_BERR_OPTIONS_EXCEED = 25,      /* options.rs:67                             */
+    ZP_BERR_ROUTING_DATA = 26,        /* builder.rs:684,719 (fragment_header too)  */
+    ZP_BERR_ROUTING_SLICE = 27,       /* routing.rs:16                             */
+    ZP_BERR_ROUTING_MIN = 28,         /* routing.rs:77                             */
+    ZP_BERR_ROUTING_MATCH = 29,       /* routing.rs:83                             */
+    ZP_BERR_ROUTING_EXCEED = 30,      /* routing.rs:90                             */
+    ZP_BERR_AUTH_DATA = 31,           /* builder.rs:756                            */
+    ZP_BERR_AUTH_SLICE = 32,          /* authentication.rs:16                      */
+    ZP_BERR_AUTH_EXCEED = 33,         /* authentication.rs:88                      */
+    ZP_BERR_PANIC = 34,               /* the reference would panic: fragment.rs:16 */
+                                      /* panic!, or a slice index out of range      */
+                                      /* (ipv4.rs:123, tcp.rs:114)                  */
+    ZP_BERR_TRANSITION = 35,          /* chain not allowed by builder.rs:817-909    */
+    ZP_BERR_COUNT = 36
+} zp_build_err;
+
+typedef struct zp_build_result {
+    uint32_t header_len;               /* PacketBuilder::header_len() (builder.rs:65) */
+    uint8_t  err;                      /* zp_build_err                             */
+    uint8_t  ops_done;                 /* ops that returned Ok                     */
+    uint16_t reserved;
+} zp_build_result;
+
+/* Exact reference string of a zp_build_err ("" for OK, NULL out of range). */
+const char* zp_build_err_str(int code);
+
+/* Runs n builder chains in place on the device. Frame i is the buffer
+ * arena[offs[i] .. offs[i] + lens[i]) (the reference's `&mut [u8]`), its
+ * chain is ops[op_start[i] .. op_start[i + 1]) (op_start has n + 1 entries),
+ * variable bytes come from `data`. results may be NULL. All pointers are
+ * device memory; enqueues on `stream`. Returns 0 or negative on failure. */
+int zp_build_batch_device(uint8_t* arena, const uint64_t* offs, const uint32_t* lens,
+                          uint64_t n, const zp_build_op* ops, const uint32_t* op_start,
+                          const uint8_t* data, zp_build_result* results, void* stream);
+
+/* ------------------------------------------------------------------------- */
 /* Synthetic batch generator (BASELINE.json configs 1-5), built from the      */
 /* builder's checksum-fill semantics (builder.rs:473-474,515-516,553,592-593).*/
 /* Deterministic per packet: packet i depends only on (config, seed, i).      */

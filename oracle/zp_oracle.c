@@ -560,3 +560,262 @@ int zpo_columns(const uint8_t* arena, const uint64_t* offs, const uint32_t* lens
     }
     return 0;
 }
+
+/* ---- PacketBuilder restatement -------------------- */
+/* builder.rs:55-909 with the writers it calls (ethernet.rs:19-129,
+ * arp.rs:7-119, ipv4.rs:8-127, ipv6.rs:8-133, options.rs / routing.rs /
+ * fragment.rs / authentication.rs writers, tcp.rs:7-130, udp.rs:7-92,
+ * icmpv4.rs:10-81, icmpv6.rs:7-78). One chain of ops over one buffer; the
+ * first Err stops the chain with its partial writes left in the buffer. */
+
+enum { ST_RAW, ST_ETH, ST_ARP, ST_V4, ST_V6, ST_HBH, ST_D1, ST_RT, ST_FR, ST_AH, ST_D2,
+       ST_V4E, ST_V6E, ST_L4 };
+
+/* builder.rs:817-909: the state after `kind` from `st`, or -1. */
+static int next_state(int st, int kind) {
+    const int l4v4 = kind == ZP_B_TCP || kind == ZP_B_UDP || kind == ZP_B_ICMPV4;
+    const int l4v6 = kind == ZP_B_TCP || kind == ZP_B_UDP || kind == ZP_B_ICMPV6;
+    switch (st) {
+    case ST_RAW:
+        return (kind == ZP_B_ETHERNET || kind == ZP_B_ETHERNET_VLAN ||
+                kind == ZP_B_ETHERNET_QINQ) ? ST_ETH : -1;
+    case ST_ETH:
+        return kind == ZP_B_ARP ? ST_ARP : kind == ZP_B_IPV4 ? ST_V4 : kind == ZP_B_IPV6 ? ST_V6 : -1;
+    case ST_V4:
+        if (l4v4) return ST_L4;
+        return kind == ZP_B_IPV4 ? ST_V4E : kind == ZP_B_IPV6 ? ST_V6E : -1;
+    case ST_V4E: return l4v4 ? ST_L4 : -1;
+    case ST_V6E: return l4v6 ? ST_L4 : -1;
+    case ST_V6: case ST_HBH: case ST_D1: case ST_RT: case ST_FR: case ST_AH: case ST_D2:
+        if (l4v6) return ST_L4;
+        if (kind == ZP_B_IPV4) return ST_V4E;
+        if (kind == ZP_B_IPV6) return ST_V6E;
+        if (kind == ZP_B_HOP_BY_HOP) return st == ST_V6 ? ST_HBH : -1;
+        if (kind == ZP_B_DEST_OPTS1) return (st == ST_V6 || st == ST_HBH) ? ST_D1 : -1;
+        if (kind == ZP_B_ROUTING) return (st == ST_V6 || st == ST_HBH || st == ST_D1) ? ST_RT : -1;
+        if (kind == ZP_B_FRAGMENT) return (st == ST_V6 || st == ST_HBH || st == ST_RT) ? ST_FR : -1;
+        if (kind == ZP_B_AUTH)
+            return (st == ST_V6 || st == ST_HBH || st == ST_RT || st == ST_FR) ? ST_AH : -1;
+        if (kind == ZP_B_DEST_OPTS2) return st != ST_D1 && st != ST_D2 ? ST_D2 : -1;
+        return -1;
+    default:
+        return -1;   /* ARP and L4 states are terminal */
+    }
+}
+
+static void wr16(uint8_t* b, size_t i, uint16_t v) { b[i] = (uint8_t)(v >> 8); b[i + 1] = (uint8_t)v; }
+static void wr32(uint8_t* b, size_t i, uint32_t v) {
+    b[i] = (uint8_t)(v >> 24); b[i + 1] = (uint8_t)(v >> 16); b[i + 2] = (uint8_t)(v >> 8); b[i + 3] = (uint8_t)v;
+}
+
+/* internet_checksum over s into bytes [at, at+2) (the writers' set_checksum). */
+static void put_csum(uint8_t* s, size_t n, size_t at, uint32_t acc) {
+    s[at] = 0;
+    s[at + 1] = 0;
+    const uint16_t c = zpo_internet_checksum(s, n, acc);
+    s[at] = (uint8_t)(c >> 8);
+    s[at + 1] = (uint8_t)(c & 0xFF);
+}
+
+int zpo_build(uint8_t* buf, size_t n, const zp_build_op* ops, uint32_t nops,
+              const uint8_t* data, zp_build_result* res) {
+    memset(res, 0, sizeof *res);
+    int st = ST_RAW;
+    for (uint32_t k = 0; k < nops; ++k) {                 /* typestate: compile-time in Rust */
+        st = next_state(st, ops[k].kind);
+        if (st < 0) { res->err = ZP_BERR_TRANSITION; return ZP_BERR_TRANSITION; }
+    }
+    st = ST_RAW;
+    size_t hl = 0;
+    for (uint32_t k = 0; k < nops; ++k) {
+        const zp_build_op* o = &ops[k];
+        const int prev = st;
+        st = next_state(st, o->kind);
+        const int has_data = o->data_len != ZP_BUILD_NO_DATA;
+        const uint8_t* d = data + o->data_off;
+        const size_t dl = has_data ? o->data_len : 0;
+        uint8_t* s = buf + hl;                           /* &mut self.bytes[self.header_len..] */
+        const size_t sl = n - hl;
+        int e = 0;
+        switch (o->kind) {
+        case ZP_B_ETHERNET: case ZP_B_ETHERNET_VLAN: case ZP_B_ETHERNET_QINQ: {
+            if (n < 14) { e = ZP_BERR_ETH_SLICE; break; }                 /* ethernet.rs:29-31 */
+            memcpy(buf + 6, o->src, 6);                                    /* set_src_mac :56-63 */
+            memcpy(buf, o->dst, 6);                                        /* set_dest_mac :45-52 */
+            size_t h = 14;
+            if (o->kind == ZP_B_ETHERNET_VLAN) {                           /* set_vlan_tag :83-96 */
+                if (n < h + 4) { e = ZP_BERR_ETH_VLAN; break; }
+                wr16(buf, 12, 0x8100); wr16(buf, 14, o->h[1]);
+                h += 4;
+            } else if (o->kind == ZP_B_ETHERNET_QINQ) {                    /* :104-128 */
+                if (n < h + 8) { e = ZP_BERR_ETH_QINQ; break; }
+                wr16(buf, 12, 0x88A8); wr16(buf, 14, o->h[1]);
+                wr16(buf, 16, 0x8100); wr16(buf, 18, o->h[2]);
+                h += 8;
+            }
+            wr16(buf, 12 + (h - 14), o->h[0]);                             /* set_ethertype :70-74 */
+            hl = h;                                                        /* builder.rs:124,155,186 */
+            break;
+        }
+        case ZP_B_ARP:                                                     /* builder.rs:203-236 */
+            if (n < hl) { e = ZP_BERR_ARP_DATA; break; }
+            if (sl < 28) { e = ZP_BERR_ARP_SLICE; break; }
+            wr16(s, 0, o->h[0]); wr16(s, 2, o->h[1]); s[4] = o->b[0]; s[5] = o->b[1];
+            wr16(s, 6, o->h[2]);
+            memcpy(s + 8, o->src, 6); memcpy(s + 14, o->src + 6, 4);
+            memcpy(s + 18, o->dst, 6); memcpy(s + 24, o->dst + 6, 4);
+            hl += 28;
+            break;
+        case ZP_B_IPV4: {                                                  /* builder.rs:248-292 */
+            if (n < hl) { e = ZP_BERR_IPV4_DATA; break; }
+            if (sl < 20) { e = ZP_BERR_IPV4_SLICE; break; }               /* ipv4.rs:17-19 */
+            s[0] = (uint8_t)((s[0] & 0x0F) | (uint8_t)(o->b[0] << 4));    /* ipv4.rs:35-38 */
+            s[0] = (uint8_t)((s[0] & 0xF0) | (o->b[1] & 0x0F));
+            s[1] = (uint8_t)((s[1] & 0x03) | (uint8_t)(o->b[2] << 2));
+            s[1] = (uint8_t)((s[1] & 0xFC) | (o->b[3] & 0x03));
+            wr16(s, 2, o->h[0]);
+            wr16(s, 4, o->h[1]);
+            s[6] = (uint8_t)((s[6] & 0x1F) | ((uint8_t)(o->b[4] << 5) & 0xE0));
+            s[6] = (uint8_t)((s[6] & 0xE0) | ((o->h[2] >> 8) & 0x1F));
+            s[7] = (uint8_t)(o->h[2] & 0xFF);
+            s[8] = o->b[5];
+            s[9] = o->b[6];
+            memcpy(s + 12, o->src, 4);
+            memcpy(s + 16, o->dst, 4);
+            const size_t ihl = (size_t)(s[0] & 0x0F) * 4;                  /* ipv4.rs:26-28 */
+            s[10] = 0; s[11] = 0;                                          /* set_checksum :119-126 */
+            if (ihl > sl) { e = ZP_BERR_PANIC; break; }                    /* &bytes[..header_len] */
+            put_csum(s, ihl, 10, 0);
+            hl += ihl;
+            break;
+        }
+        case ZP_B_IPV6:                                                    /* builder.rs:300-335 */
+            if (n < hl) { e = ZP_BERR_IPV6_DATA; break; }
+            if (sl < 40) { e = ZP_BERR_IPV6_SLICE; break; }
+            s[0] = (uint8_t)((s[0] & 0x0F) | (uint8_t)(o->b[0] << 4));    /* ipv6.rs:33-36 */
+            s[0] = (uint8_t)((s[0] & 0xF0) | (o->b[1] >> 4));             /* :40-44 */
+            s[1] = (uint8_t)((s[1] & 0x0F) | (uint8_t)(o->b[1] << 4));
+            s[1] = (uint8_t)((s[1] & 0xF0) | (uint8_t)(o->w[0] >> 16));   /* :48-52 (unmasked) */
+            s[2] = (uint8_t)(o->w[0] >> 8);
+            s[3] = (uint8_t)o->w[0];
+            wr16(s, 4, o->h[0]);
+            s[6] = o->b[2];
+            s[7] = o->b[3];
+            memcpy(s + 8, o->src, 16);
+            memcpy(s + 24, o->dst, 16);
+            hl += 40;
+            break;
+        case ZP_B_HOP_BY_HOP: case ZP_B_DEST_OPTS1: case ZP_B_DEST_OPTS2: { /* builder.rs:611-806 */
+            if (n < hl) { e = o->kind == ZP_B_HOP_BY_HOP ? ZP_BERR_HBH_DATA : ZP_BERR_DEST_DATA; break; }
+            if (sl < 8) { e = ZP_BERR_OPTIONS_SLICE; break; }             /* options.rs:17-19 */
+            s[0] = o->b[0];
+            s[1] = o->b[1];
+            if (dl < 6) { e = ZP_BERR_OPTIONS_MIN; break; }               /* options.rs:53-68 */
+            if ((size_t)s[1] * 8 != dl) { e = ZP_BERR_OPTIONS_MATCH; break; }
+            if (2 + dl > sl) { e = ZP_BERR_OPTIONS_EXCEED; break; }
+            memcpy(s + 2, d, dl);
+            hl += ((size_t)s[1] + 1) * 8;
+            break;
+        }
+        case ZP_B_ROUTING:                                                 /* builder.rs:675-704 */
+            if (n < hl) { e = ZP_BERR_ROUTING_DATA; break; }
+            if (sl < 8) { e = ZP_BERR_ROUTING_SLICE; break; }
+            s[0] = o->b[0]; s[1] = o->b[1]; s[2] = o->b[2]; s[3] = o->b[3];
+            if (dl < 4) { e = ZP_BERR_ROUTING_MIN; break; }               /* routing.rs:75-94 */
+            if ((size_t)s[1] * 8 != dl) { e = ZP_BERR_ROUTING_MATCH; break; }
+            if (8 + dl > sl) { e = ZP_BERR_ROUTING_EXCEED; break; }
+            memcpy(s + 8, d, dl);
+            hl += ((size_t)s[1] + 1) * 8;
+            break;
+        case ZP_B_FRAGMENT: {                                              /* builder.rs:711-740 */
+            if (n < hl) { e = ZP_BERR_ROUTING_DATA; break; }              /* (its message) */
+            if (sl < 8) { e = ZP_BERR_PANIC; break; }                     /* fragment.rs:15-17 panic! */
+            s[0] = o->b[0];
+            s[1] = 0;
+            const uint16_t v = o->h[0] & 0x1FFF;                          /* fragment.rs:52-57 */
+            s[2] = (uint8_t)(v >> 5);
+            s[3] = (uint8_t)((s[3] & 0xE0) | (v & 0x1F));
+            s[3] = (uint8_t)(s[3] & 0x9F);                                /* set_res(0) */
+            if (o->b[1]) s[3] |= 0x80; else s[3] &= 0x7F;                 /* set_m_flag */
+            wr32(s, 4, o->w[0]);
+            hl += 8;
+            break;
+        }
+        case ZP_B_AUTH:                                                    /* builder.rs:747-778 */
+            if (n < hl) { e = ZP_BERR_AUTH_DATA; break; }
+            if (sl < 12) { e = ZP_BERR_AUTH_SLICE; break; }
+            s[0] = o->b[0]; s[1] = o->b[1]; s[2] = 0; s[3] = 0;
+            wr32(s, 4, o->w[0]);
+            wr32(s, 8, o->w[1]);
+            if (12 + dl > sl) { e = ZP_BERR_AUTH_EXCEED; break; }         /* authentication.rs:84-92 */
+            memcpy(s + 12, d, dl);
+            hl += ((size_t)s[1] + 2) * 4;
+            break;
+        case ZP_B_TCP: case ZP_B_UDP: case ZP_B_ICMPV4: case ZP_B_ICMPV6: {
+            const int v4 = prev == ST_V4 || prev == ST_V4E;               /* &[u8; 4] states */
+            if (n < hl) {
+                e = o->kind == ZP_B_TCP ? ZP_BERR_TCP_DATA : o->kind == ZP_B_UDP ? ZP_BERR_UDP_DATA
+                  : o->kind == ZP_B_ICMPV4 ? ZP_BERR_ICMPV4_DATA : ZP_BERR_ICMPV6_DATA;
+                break;
+            }
+            size_t start;
+            if (o->kind == ZP_B_TCP) {                                     /* builder.rs:438-485 */
+                if (sl < 20) { e = ZP_BERR_TCP_SLICE; break; }
+                wr16(s, 0, o->h[0]); wr16(s, 2, o->h[1]);
+                wr32(s, 4, o->w[0]); wr32(s, 8, o->w[1]);
+                s[12] = (uint8_t)((uint8_t)(o->b[0] << 4) | (s[12] & 0x0F));
+                s[12] = (uint8_t)((s[12] & 0xF0) | (o->b[1] & 0x0F));
+                s[13] = o->b[2];
+                wr16(s, 14, o->h[2]);
+                wr16(s, 18, o->h[3]);
+                start = (size_t)(s[12] >> 4) * 4;
+            } else if (o->kind == ZP_B_UDP) {                              /* builder.rs:492-527 */
+                if (sl < 8) { e = ZP_BERR_UDP_SLICE; break; }
+                wr16(s, 0, o->h[0]); wr16(s, 2, o->h[1]); wr16(s, 4, o->h[2]);
+                start = 8;
+            } else {                                                       /* builder.rs:534-604 */
+                if (sl < 8) { e = ZP_BERR_ICMP_SLICE; break; }
+                s[0] = o->b[0]; s[1] = o->b[1];
+                start = 8;
+            }
+            if (has_data) {                                                /* set_payload */
+                if (start > sl) { e = ZP_BERR_PANIC; break; }              /* tcp.rs:109-114: wrap, then slice panic */
+                if (sl - start < dl) {
+                    e = o->kind == ZP_B_ICMPV4 ? ZP_BERR_ICMPV4_PAYLOAD
+                      : o->kind == ZP_B_ICMPV6 ? ZP_BERR_ICMPV6_PAYLOAD : ZP_BERR_TCP_PAYLOAD;
+                    break;
+                }
+                memcpy(s + start, d, dl);
+            }
+            uint32_t acc = 0;
+            const uint8_t proto = o->kind == ZP_B_TCP ? 6 : o->kind == ZP_B_UDP ? 17 : 58;
+            if (o->kind != ZP_B_ICMPV4)                                    /* checksum.rs:66-69 */
+                acc = zpo_pseudo_header(o->src, o->dst, v4 ? 4 : 16, proto, sl);
+            const size_t at = o->kind == ZP_B_TCP ? 16 : o->kind == ZP_B_UDP ? 6 : 2;
+            put_csum(s, sl, at, acc);
+            hl += o->kind == ZP_B_TCP ? start : 8;
+            break;
+        }
+        default:
+            e = ZP_BERR_TRANSITION;
+        }
+        if (e) {
+            res->err = (uint8_t)e;
+            res->header_len = (uint32_t)hl;
+            res->ops_done = (uint8_t)(k > 255 ? 255 : k);
+            return e;
+        }
+        res->ops_done = (uint8_t)(k + 1 > 255 ? 255 : k + 1);
+    }
+    res->header_len = (uint32_t)hl;
+    return 0;
+}
+
+int zpo_build_batch(uint8_t* arena, const uint64_t* offs, const uint32_t* lens, uint64_t n,
+                    const zp_build_op* ops, const uint32_t* op_start, const uint8_t* data,
+                    zp_build_result* res) {
+    for (uint64_t i = 0; i < n; ++i)
+        zpo_build(arena + offs[i], lens[i], ops + op_start[i], op_start[i + 1] - op_start[i],
+                  data, &res[i]);
+    return 0;
+}

@@ -110,3 +110,20 @@ def columns(arena, offs, lens, recs):
         l.zpo_columns(arena.ctypes.data, offs.ctypes.data, lens.ctypes.data, recs.ctypes.data,
                       n, ptrs)
     return out
+
+
+def build_batch(arena, offs, lens, ops, op_start, data):
+    """zpo_build_batch: the PacketBuilder restatement, in place on `arena`
+    (numpy uint8, modified); returns results as uint8 [n, 8]."""
+    n = len(offs)
+    res = np.zeros((n, 8), np.uint8)
+    l = lib()
+    l.zpo_build_batch.restype = ctypes.c_int
+    l.zpo_build_batch.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_uint64] + [ctypes.c_void_p] * 4
+    offs = np.ascontiguousarray(offs, np.uint64)
+    lens = np.ascontiguousarray(lens, np.uint32)
+    if n:
+        l.zpo_build_batch(arena.ctypes.data, offs.ctypes.data, lens.ctypes.data, n,
+                          ops.ctypes.data, op_start.ctypes.data, data.ctypes.data,
+                          res.ctypes.data)
+    return res

@@ -7,6 +7,7 @@ Import with importlib (the directory name has a hyphen):
   zp.batch.generate(cfg, n)                  synthetic BASELINE configs on the GPU
   zp.columns.extract(arena, offs, lens, recs) reader getters as SoA device columns
   zp.ring.Ring(device, slots, slot_bytes)    host-ring ingestion (H2D/parse/D2H in flight)
+  zp.builder.Chain / BuildBatch              batched PacketBuilder chains on the GPU
   zp.PacketParser.parse(frame)               one frame through the GPU path
   zp.PacketParser.from_record(frame, rec)    reference-shaped views over a record
 """
@@ -17,8 +18,8 @@ from .parser import (ArpReader, AuthenticationHeaderReader, EthernetReader,  # n
                      RoutingHeaderReader, TcpReader, UdpReader, ZeroPacketError)
 
 try:  # torch-dependent batch API
-    from . import batch, columns  # noqa: F401
+    from . import batch, builder, columns  # noqa: F401
 except ImportError:  # pragma: no cover
-    batch = columns = None
+    batch = builder = columns = None
 
 __all__ = ["PacketParser", "ZeroPacketError", "batch", "records"]
