@@ -1,0 +1,125 @@
+"""Batched PacketBuilder throughput + full-size build -> parse round trip.
+
+    python tools/build_bench.py [--frames 4194304] [--config c3]
+
+Frames of a generated batch are rebuilt in place by chains
+ethernet -> ipv4 -> tcp|udp|icmpv4 (payload None: the bytes already in the
+buffer are the payload, so the chain writes headers and checksums only) with
+fresh random header fields; every rebuilt frame must then parse Ok through
+the parse kernel (the checksums the builder wrote verify). Algorithmic bytes
+per frame: the frame is read once (the L4 checksum covers it) and the header
+bytes are written.
+"""
+import argparse
+import importlib
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, default=1 << 22)
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--variants", default="", help="tools/variants/libzb_<name>.so builds to A/B")
+    args = ap.parse_args()
+    zp = importlib.import_module("zero-packet_amd")
+    B = zp.builder
+    d = torch.device("cuda:0")
+    n = args.frames
+    arena, offs, lens = zp.batch.generate("c3", n, device=d)
+    ln = lens.cpu().numpy().astype(np.int64)
+    rng = np.random.default_rng(7)
+    ops = np.zeros(3 * n, B.OP_DTYPE)
+    eth, ip, l4 = ops[0::3], ops[1::3], ops[2::3]
+    eth["kind"] = B.ETHERNET
+    eth["src"][:, :6] = rng.integers(0, 256, (n, 6), dtype=np.uint8)
+    eth["dst"][:, :6] = rng.integers(0, 256, (n, 6), dtype=np.uint8)
+    eth["h"][:, 0] = 0x0800
+    ip["kind"] = B.IPV4
+    ip["b"][:, 0] = 4
+    ip["b"][:, 1] = 5
+    ip["b"][:, 5] = 64
+    ip["h"][:, 0] = (ln - 14).astype(np.uint16)
+    ip["h"][:, 1] = rng.integers(0, 65536, n, dtype=np.uint16)
+    ip["src"][:, :4] = rng.integers(0, 256, (n, 4), dtype=np.uint8)
+    ip["dst"][:, :4] = rng.integers(0, 256, (n, 4), dtype=np.uint8)
+    which = rng.integers(0, 3, n)
+    kinds = np.array([B.TCP, B.UDP, B.ICMPV4])[which]
+    protos = np.array([6, 17, 1])[which]
+    ip["b"][:, 6] = protos
+    l4["kind"] = kinds
+    l4["src"][:, :4] = ip["src"][:, :4]
+    l4["dst"][:, :4] = ip["dst"][:, :4]
+    l4["h"][:, 0] = rng.integers(1, 65536, n, dtype=np.uint16)
+    l4["h"][:, 1] = rng.integers(1, 65536, n, dtype=np.uint16)
+    tcp = which == 0
+    l4["w"][tcp, 0] = rng.integers(0, 1 << 32, int(tcp.sum()), dtype=np.uint32)
+    l4["b"][tcp, 0] = 5
+    l4["b"][tcp, 2] = 0x18
+    l4["h"][tcp, 2] = 65535
+    udp = which == 1
+    l4["h"][udp, 2] = (ln[udp] - 34).astype(np.uint16)
+    icmp = which == 2
+    l4["b"][icmp, 0] = 8
+    l4["b"][icmp, 1] = 0
+    l4["h"][icmp, 0] = 0
+    l4["h"][icmp, 1] = 0
+    for o in (eth, ip, l4):
+        o["data_len"] = B.NO_DATA
+    t_ops = torch.from_numpy(ops.view(np.uint8)).to(d)
+    t_start = torch.arange(0, 3 * n + 1, 3, dtype=torch.int32, device=d)
+    t_data = torch.zeros(16, dtype=torch.uint8, device=d)
+    res = torch.zeros((n, 8), dtype=torch.uint8, device=d)
+    import ctypes
+    libs = [("base", zp._lib.hip())]
+    for v in [x for x in args.variants.split(",") if x]:
+        l_ = ctypes.CDLL(os.path.join(ROOT, "tools", "variants", f"libzb_{v}.so"))
+        l_.zp_build_batch_device.restype = ctypes.c_int
+        l_.zp_build_batch_device.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_uint64] + \
+            [ctypes.c_void_p] * 5
+        libs.append((v, l_))
+    s = torch.cuda.current_stream(d)
+    snapshot = arena.clone()
+    errs = 0
+    ref = None
+    for name, lib in libs:
+        def launch():
+            zp._lib.check(lib.zp_build_batch_device(arena.data_ptr(), offs.data_ptr(),
+                                                    lens.data_ptr(), n, t_ops.data_ptr(),
+                                                    t_start.data_ptr(), t_data.data_ptr(),
+                                                    res.data_ptr(), s.cuda_stream),
+                          "zp_build_batch_device")
+        arena.copy_(snapshot)
+        launch()
+        torch.cuda.synchronize()
+        if ref is None:
+            ref = arena.clone()
+        elif not torch.equal(ref, arena):
+            print(f"  !! {name}: built bytes differ from base", flush=True)
+        errs += int((res[:, 4] != 0).sum())
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(args.reps)]
+        for a, b in ev:
+            a.record(s); launch(); b.record(s)
+        torch.cuda.synchronize()
+        ms = float(np.median([a.elapsed_time(b) for a, b in ev]))
+        nbytes = int(ln.sum())
+        hdr = n * 54
+        print(f"build c3 x {n} [{name}]: {ms:.3f} ms  {n / ms / 1e3:.0f} Mpkt/s  "
+              f"{(nbytes + hdr) / ms / 1e6:.0f} GB/s (frame read + header write)  errors {errs}",
+              flush=True)
+    recs, _ = zp.batch.parse_batch(arena, offs, lens)
+    torch.cuda.synchronize()
+    bad = int((recs[:, 4] != 0).sum())
+    print(f"round trip: {n - bad}/{n} rebuilt frames parse Ok", flush=True)
+    assert errs == 0 and bad == 0
+
+
+if __name__ == "__main__":
+    main()

@@ -8,6 +8,11 @@ build() {  # name flags...
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared "$@" \
      -o tools/variants/libzp_$name.so $C/zp_parse.hip || exit 1
 }
+buildb() {  # builder variants: name flags...
+  local name=$1; shift
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared "$@" \
+     -o tools/variants/libzb_$name.so $C/zp_build.hip $C/zp_parse.hip || exit 1
+}
 for v in "$@"; do
   case $v in
     nostream)   build nostream -DZP_ABL_STREAM_OFF ;;
@@ -15,6 +20,7 @@ for v in "$@"; do
     streamonly) build streamonly -DZP_ABL_FAKE_WALK -DZP_ABL_WIN_OFF ;;
     unroll8)    build unroll8 -DZP_UNROLL=8 ;;
     unroll2)    build unroll2 -DZP_UNROLL=2 ;;
+    b-*) name=${v%%:*}; flags=${v#*:}; buildb "${name#b-}" $flags ;;
     *) name=${v%%:*}; flags=${v#*:}; build "$name" $flags ;;
   esac
 done

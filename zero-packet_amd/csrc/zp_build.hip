@@ -7,12 +7,13 @@
 // tcp.rs:7-130, UdpWriter udp.rs:7-92, Icmpv4Writer icmpv4.rs:10-81,
 // Icmpv6Writer icmpv6.rs:7-78; checksums checksum.rs:5-69.
 //
-// One wave per frame (a chain is a serial program, but its payload copy and
-// the L4 checksum over the rest of the buffer are wave-wide work). Frames up
-// to ZB_CAP bytes (+ alignment) are staged in LDS: the wave loads the frame,
-// executes the chain on the LDS copy and writes back only the bytes the chain
-// can have changed. Longer frames run in place in global memory, every lane
-// executing the same chain on the same bytes.
+// One group of ZB_G lanes per frame, 64 / ZB_G frames per wave side by side:
+// a chain is a serial program (every lane of the group runs it), its payload
+// copy and the L4 checksum over the rest of the buffer are group-wide work.
+// Frames up to ZB_CAP bytes (+ alignment) are staged in LDS with the chain's
+// ops in one round trip: the group executes the chain on the LDS copy and
+// writes back only the bytes the chain can have changed. Longer frames run
+// in place in global memory, every lane of the group on the same bytes.
 //
 // The chain's scalar steps run on every lane with identical values (every
 // lane stores the same byte to the same address), so each lane reads back
@@ -28,8 +29,17 @@
 extern "C" char* zp__errbuf(void);
 
 #define ZB_WAVES 4
-#define ZB_CAP 2048            // frame bytes staged in LDS per wave
+#ifndef ZB_CAP
+#define ZB_CAP 1536            // frame bytes staged in LDS per frame
+#endif
 #define ZB_LDS (ZB_CAP + 32)   // + the frame's offset in its first 16-B chunk
+#ifndef ZB_OPS
+#define ZB_OPS 8               // ops of a chain prefetched to LDS (longer chains read the rest)
+#endif
+#ifndef ZB_G
+#define ZB_G 16                // lanes per frame: a wave builds 64 / ZB_G frames side by side
+#endif
+#define ZB_F (64 / ZB_G)       // frames per wave
 
 // Exact reference strings (see zero_packet.h for the cited lines).
 static const char* const kBuildErr[ZP_BERR_COUNT] = {
@@ -106,27 +116,41 @@ __device__ __forceinline__ int bnext(int st, int k) {
     }
 }
 
-// Frame view for the chain: a generic pointer to the staged (LDS) or the
-// in-place (global) bytes. Every lane executes every access.
+// Frame view for the chain. Every lane executes the chain's stores with the
+// same values and reads back its own stores: no cross-lane dependency through
+// memory outside the cooperative steps, which end in wave_sync(). (Stores by
+// lane 0 alone read by the other lanes would be a data race: the compiler may
+// forward a lane's earlier load past another lane's store.)
+// LDS mode (P = LDS pointer): copies and the checksum are lane-strided.
+// Global mode (P = generic pointer to the frame in place, frames past the
+// LDS size): every lane runs everything on the same bytes.
+#define ZB_LDSP __attribute__((address_space(3)))
+typedef unsigned zb_u32x4 __attribute__((ext_vector_type(4)));
+
+template <typename P>
 struct BView {
-    uint8_t* b;
+    P b;
     uint32_t n;
-    uint32_t hw;      // one past the highest byte written (LDS write-back bound)
+    bool writer;      // this lane stores
 };
 
-__device__ __forceinline__ void w8(BView& v, uint32_t i, uint32_t x) {
-    v.b[i] = (uint8_t)x;
-    v.hw = i + 1 > v.hw ? i + 1 : v.hw;
+template <typename P>
+__device__ __forceinline__ void w8(BView<P>& v, uint32_t i, uint32_t x) {
+    if (v.writer) v.b[i] = (uint8_t)x;
 }
-__device__ __forceinline__ void w16(BView& v, uint32_t i, uint32_t x) {
+template <typename P>
+__device__ __forceinline__ void w16(BView<P>& v, uint32_t i, uint32_t x) {
     w8(v, i, x >> 8);
     w8(v, i + 1, x);
 }
-__device__ __forceinline__ void w32(BView& v, uint32_t i, uint32_t x) {
+template <typename P>
+__device__ __forceinline__ void w32(BView<P>& v, uint32_t i, uint32_t x) {
     w16(v, i, x >> 16);
     w16(v, i + 2, x);
 }
-__device__ __forceinline__ void wbytes(BView& v, uint32_t i, const uint8_t* s, int k) {
+template <typename P>
+__device__ __forceinline__ void wbytes(BView<P>& v, uint32_t i, const uint8_t* s, int k) {
+#pragma unroll
     for (int q = 0; q < k; ++q) w8(v, i + q, s[q]);
 }
 
@@ -136,73 +160,130 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Copies `len` bytes of the data blob to frame offset `at`: lane-strided in
-// LDS mode (then a wave barrier), every lane all bytes in global mode.
-__device__ void bcopy(BView& v, uint32_t at, const uint8_t* src, uint32_t len, bool coop,
-                      int lane) {
-    if (coop) {
-        for (uint32_t q = lane; q < len; q += 64) v.b[at + q] = src[q];
+// Copies `len` bytes of the data blob to frame offset `at`.
+template <bool COOP, typename P>
+__device__ void bcopy(BView<P>& v, uint32_t at, const uint8_t* src, uint32_t len, int lane) {
+    if (COOP) {
+        for (uint32_t q = lane; q < len; q += ZB_G) v.b[at + q] = src[q];
         wave_sync();
     } else {
         for (uint32_t q = 0; q < len; ++q) v.b[at + q] = src[q];
     }
-    if (len) v.hw = at + len > v.hw ? at + len : v.hw;
 }
 
-// internet_checksum(bytes[s0 .. n], acc) (checksum.rs:5-29, u32 wrap): the
-// u32 sum is associative, so a lane-strided partial sum + wave reduction is
-// bit-identical to the reference's sequential loop.
-__device__ uint16_t bcsum(const BView& v, uint32_t s0, uint32_t acc, bool coop, int lane) {
-    const uint32_t len = v.n - s0;
-    const uint32_t words = len >> 1;
-    uint32_t sum = 0;
-    const uint32_t first = coop ? (uint32_t)lane : 0u, step = coop ? 64u : 1u;
-    for (uint32_t w = first; w < words; w += step)
-        sum += ((uint32_t)v.b[s0 + 2 * w] << 8) | v.b[s0 + 2 * w + 1];
-    if (coop) {
+// S = acc + sum of big-endian words of bytes[s0 .. n) (checksum.rs:11-20; a
+// trailing odd byte counts as its high byte), folded and inverted
+// (checksum.rs:23-28). Exact: the word sum is 256 * (bytes at even positions
+// from s0) + (bytes at odd positions), both plain byte sums.
+// LDS mode: `stage` is the wave's staging buffer and `shift` the frame's
+// offset in it; each lane sums whole 16-B cells with v_sad_u8 over
+// even/odd-address byte masks, then a wave reduction.
+__device__ uint16_t bcsum_lds(const uint8_t ZB_LDSP* stage, uint32_t shift, uint32_t s0,
+                              uint32_t n, uint32_t acc, int lane) {
+    const uint32_t p0 = shift + s0, p1 = shift + n;      // staged byte range
+    uint32_t ev = 0, od = 0;                             // bytes at even / odd staged positions
+    for (uint32_t c = (p0 >> 4) + lane; 16 * c < p1; c += ZB_G) {
+        const zb_u32x4 q = *(const zb_u32x4 ZB_LDSP*)(stage + 16 * c);
+        const uint32_t d[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1) sum += (uint32_t)__shfl_xor((int)sum, off);
+        for (int k = 0; k < 4; ++k) {
+            const int base = (int)(16 * c + 4 * k);
+            const int lo = (int)p0 - base, hi = (int)p1 - base;
+            const uint32_t a = lo < 0 ? 0u : (lo > 4 ? 4u : (uint32_t)lo);
+            const uint32_t b = hi < 0 ? 0u : (hi > 4 ? 4u : (uint32_t)hi);
+            const uint32_t m = (uint32_t)(0xFFFFFFFFull >> (32 - 8 * b)) &
+                               ~(uint32_t)(0xFFFFFFFFull >> (32 - 8 * a));
+            const uint32_t x = d[k] & m;
+            ev = __builtin_amdgcn_sad_u8(x & 0x00FF00FFu, 0u, ev);
+            od = __builtin_amdgcn_sad_u8(x & 0xFF00FF00u, 0u, od);
+        }
     }
-    sum += acc;
-    if (len & 1) sum += (uint32_t)v.b[v.n - 1] << 8;
+#pragma unroll
+    for (int off = ZB_G / 2; off > 0; off >>= 1) {     // within the frame's lane group
+        ev += (uint32_t)__shfl_xor((int)ev, off);
+        od += (uint32_t)__shfl_xor((int)od, off);
+    }
+    uint32_t sum = acc + ((p0 & 1) ? 256u * od + ev : 256u * ev + od);
     while (sum >> 16) sum = (sum & 0xFFFF) + (sum >> 16);
     return (uint16_t)~sum;
 }
 
-// checksum.rs:43-69 over 4- or 16-byte addresses.
-__device__ __forceinline__ uint32_t pseudo(const zp_build_op& o, int alen, uint32_t proto,
-                                           uint32_t length) {
-    uint32_t s = 0;
-    for (int k = 0; k < alen; k += 2) s += ((uint32_t)o.src[k] << 8) | o.src[k + 1];
-    for (int k = 0; k < alen; k += 2) s += ((uint32_t)o.dst[k] << 8) | o.dst[k + 1];
-    return s + proto + length;
+// Global mode: the reference's sequential loop (u32 wrap included).
+__device__ uint16_t bcsum_seq(const uint8_t* b, uint32_t s0, uint32_t n, uint32_t acc) {
+    uint32_t sum = acc;
+    uint32_t i = s0;
+    for (; i + 1 < n; i += 2) sum += ((uint32_t)b[i] << 8) | b[i + 1];
+    if (i < n) sum += (uint32_t)b[i] << 8;
+    while (sum >> 16) sum = (sum & 0xFFFF) + (sum >> 16);
+    return (uint16_t)~sum;
 }
 
+// checksum.rs:43-69 over 4- or 16-byte addresses (constant indices only).
+__device__ __forceinline__ uint32_t pseudo(const zp_build_op& o, bool v4, uint32_t proto,
+                                           uint32_t length) {
+    uint32_t s4 = 0, s16 = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k += 2) {
+        const uint32_t w = (((uint32_t)o.src[k] << 8) | o.src[k + 1]) +
+                           (((uint32_t)o.dst[k] << 8) | o.dst[k + 1]);
+        s16 += w;
+        if (k < 4) s4 += w;
+    }
+    return (v4 ? s4 : s16) + proto + length;
+}
+
+// Op k of the chain: the first ZB_OPS from the wave's LDS copy (fetched with
+// the frame in one round trip), the rest from global memory.
+struct OpSrc {
+    const zp_build_op ZB_LDSP* lds;
+    const zp_build_op* g;
+    __device__ __forceinline__ zp_build_op get(uint32_t k) const {
+        if (k < ZB_OPS) {
+            zp_build_op o;
+            const zb_u32x4 ZB_LDSP* q = (const zb_u32x4 ZB_LDSP*)(lds + k);
+            zb_u32x4 t[4] = {q[0], q[1], q[2], q[3]};
+            __builtin_memcpy(&o, t, sizeof o);
+            return o;
+        }
+        return g[k];
+    }
+    __device__ __forceinline__ uint32_t kind(uint32_t k) const {
+        return k < ZB_OPS ? lds[k].kind : g[k].kind;
+    }
+};
+
 // Executes one chain (all checks of the reference, in its order). Returns
-// the zp_build_err; *hl_out = header_len after the last Ok op.
-__device__ int run_chain(BView& v, const zp_build_op* __restrict__ ops, uint32_t nops,
-                         const uint8_t* __restrict__ data, bool coop, int lane, uint32_t* hl_out,
-                         uint32_t* done_out) {
+// the zp_build_err; *hl_out = header_len after the last Ok op, *hw_out = an
+// upper bound of the bytes written ([0, hw)).
+template <bool COOP, typename P>
+__device__ int run_chain(BView<P>& v, const uint8_t ZB_LDSP* stage, uint32_t shift,
+                         const OpSrc& ops, uint32_t nops,
+                         const uint8_t* __restrict__ data, int lane, uint32_t* hl_out,
+                         uint32_t* done_out, uint32_t* hw_out) {
     int st = BS_RAW;
+    *hw_out = 0;
     for (uint32_t k = 0; k < nops; ++k) {            // typestate (compile time in Rust)
-        st = bnext(st, ops[k].kind);
+        st = bnext(st, (int)ops.kind(k));
         if (st < 0) { *hl_out = 0; *done_out = 0; return ZP_BERR_TRANSITION; }
     }
     st = BS_RAW;
-    uint32_t hl = 0;
+    uint32_t hl = 0, hw = 0;
     const uint32_t n = v.n;
     for (uint32_t k = 0; k < nops; ++k) {
-        const zp_build_op o = ops[k];
+        const zp_build_op o = ops.get(k);
         const int prev = st;
         st = bnext(st, o.kind);
         const bool has = o.data_len != ZP_BUILD_NO_DATA;
         const uint32_t dl = has ? o.data_len : 0u;
         const uint8_t* d = data + o.data_off;
         const uint32_t sl = n - hl;                  // &mut bytes[header_len..]
-        uint8_t* s = v.b + hl;
+        const uint32_t base = hl;
+        P s = v.b + hl;
+        uint32_t ext = 0;                            // bytes this op may write from `base`
         int e = 0;
         switch (o.kind) {
         case ZP_B_ETHERNET: case ZP_B_ETHERNET_VLAN: case ZP_B_ETHERNET_QINQ: {
+            ext = 22;
             if (n < 14) { e = ZP_BERR_ETH_SLICE; break; }               // ethernet.rs:29-31
             wbytes(v, 6, o.src, 6);                                      // set_src_mac
             wbytes(v, 0, o.dst, 6);                                      // set_dest_mac
@@ -222,6 +303,7 @@ __device__ int run_chain(BView& v, const zp_build_op* __restrict__ ops, uint32_t
             break;
         }
         case ZP_B_ARP:                                                   // builder.rs:203-236
+            ext = 28;
             if (n < hl) { e = ZP_BERR_ARP_DATA; break; }
             if (sl < 28) { e = ZP_BERR_ARP_SLICE; break; }
             w16(v, hl, o.h[0]); w16(v, hl + 2, o.h[1]); w8(v, hl + 4, o.b[0]); w8(v, hl + 5, o.b[1]);
@@ -231,6 +313,7 @@ __device__ int run_chain(BView& v, const zp_build_op* __restrict__ ops, uint32_t
             hl += 28;
             break;
         case ZP_B_IPV4: {                                                // builder.rs:248-292
+            ext = 20;
             if (n < hl) { e = ZP_BERR_IPV4_DATA; break; }
             if (sl < 20) { e = ZP_BERR_IPV4_SLICE; break; }
             w8(v, hl, (s[0] & 0x0F) | (uint8_t)(o.b[0] << 4));          // ipv4.rs:33-72
@@ -257,6 +340,7 @@ __device__ int run_chain(BView& v, const zp_build_op* __restrict__ ops, uint32_t
             break;
         }
         case ZP_B_IPV6:                                                  // builder.rs:300-335
+            ext = 40;
             if (n < hl) { e = ZP_BERR_IPV6_DATA; break; }
             if (sl < 40) { e = ZP_BERR_IPV6_SLICE; break; }
             w8(v, hl, (s[0] & 0x0F) | (uint8_t)(o.b[0] << 4));          // ipv6.rs:33-61
@@ -273,6 +357,7 @@ __device__ int run_chain(BView& v, const zp_build_op* __restrict__ ops, uint32_t
             hl += 40;
             break;
         case ZP_B_HOP_BY_HOP: case ZP_B_DEST_OPTS1: case ZP_B_DEST_OPTS2: // builder.rs:611-806
+            ext = 2 + dl;
             if (n < hl) { e = o.kind == ZP_B_HOP_BY_HOP ? ZP_BERR_HBH_DATA : ZP_BERR_DEST_DATA; break; }
             if (sl < 8) { e = ZP_BERR_OPTIONS_SLICE; break; }
             w8(v, hl, o.b[0]);
@@ -280,20 +365,22 @@ __device__ int run_chain(BView& v, const zp_build_op* __restrict__ ops, uint32_t
             if (dl < 6) { e = ZP_BERR_OPTIONS_MIN; break; }             // options.rs:53-68
             if ((uint32_t)s[1] * 8 != dl) { e = ZP_BERR_OPTIONS_MATCH; break; }
             if (2 + dl > sl) { e = ZP_BERR_OPTIONS_EXCEED; break; }
-            bcopy(v, hl + 2, d, dl, coop, lane);
+            bcopy<COOP>(v, hl + 2, d, dl, lane);
             hl += ((uint32_t)s[1] + 1) * 8;
             break;
         case ZP_B_ROUTING:                                               // builder.rs:675-704
+            ext = 8 + dl;
             if (n < hl) { e = ZP_BERR_ROUTING_DATA; break; }
             if (sl < 8) { e = ZP_BERR_ROUTING_SLICE; break; }
             w8(v, hl, o.b[0]); w8(v, hl + 1, o.b[1]); w8(v, hl + 2, o.b[2]); w8(v, hl + 3, o.b[3]);
             if (dl < 4) { e = ZP_BERR_ROUTING_MIN; break; }             // routing.rs:75-94
             if ((uint32_t)s[1] * 8 != dl) { e = ZP_BERR_ROUTING_MATCH; break; }
             if (8 + dl > sl) { e = ZP_BERR_ROUTING_EXCEED; break; }
-            bcopy(v, hl + 8, d, dl, coop, lane);
+            bcopy<COOP>(v, hl + 8, d, dl, lane);
             hl += ((uint32_t)s[1] + 1) * 8;
             break;
         case ZP_B_FRAGMENT: {                                            // builder.rs:711-740
+            ext = 8;
             if (n < hl) { e = ZP_BERR_ROUTING_DATA; break; }            // (its message)
             if (sl < 8) { e = ZP_BERR_PANIC; break; }                   // fragment.rs:15-17
             w8(v, hl, o.b[0]);
@@ -308,17 +395,19 @@ __device__ int run_chain(BView& v, const zp_build_op* __restrict__ ops, uint32_t
             break;
         }
         case ZP_B_AUTH:                                                  // builder.rs:747-778
+            ext = 12 + dl;
             if (n < hl) { e = ZP_BERR_AUTH_DATA; break; }
             if (sl < 12) { e = ZP_BERR_AUTH_SLICE; break; }
             w8(v, hl, o.b[0]); w8(v, hl + 1, o.b[1]); w8(v, hl + 2, 0); w8(v, hl + 3, 0);
             w32(v, hl + 4, o.w[0]);
             w32(v, hl + 8, o.w[1]);
             if (12 + dl > sl) { e = ZP_BERR_AUTH_EXCEED; break; }       // authentication.rs:84-92
-            bcopy(v, hl + 12, d, dl, coop, lane);
+            bcopy<COOP>(v, hl + 12, d, dl, lane);
             hl += ((uint32_t)s[1] + 2) * 4;
             break;
         case ZP_B_TCP: case ZP_B_UDP: case ZP_B_ICMPV4: case ZP_B_ICMPV6: {
             const bool v4 = prev == BS_V4 || prev == BS_V4E;            // &[u8; 4] states
+            ext = 20;
             if (n < hl) {
                 e = o.kind == ZP_B_TCP ? ZP_BERR_TCP_DATA : o.kind == ZP_B_UDP ? ZP_BERR_UDP_DATA
                   : o.kind == ZP_B_ICMPV4 ? ZP_BERR_ICMPV4_DATA : ZP_BERR_ICMPV6_DATA;
@@ -351,14 +440,20 @@ __device__ int run_chain(BView& v, const zp_build_op* __restrict__ ops, uint32_t
                       : o.kind == ZP_B_ICMPV6 ? ZP_BERR_ICMPV6_PAYLOAD : ZP_BERR_TCP_PAYLOAD;
                     break;
                 }
-                bcopy(v, hl + start, d, dl, coop, lane);
+                ext = start + dl > ext ? start + dl : ext;
+                bcopy<COOP>(v, hl + start, d, dl, lane);
             }
             const uint32_t proto = o.kind == ZP_B_TCP ? 6u : o.kind == ZP_B_UDP ? 17u : 58u;
-            const uint32_t acc = o.kind == ZP_B_ICMPV4 ? 0u : pseudo(o, v4 ? 4 : 16, proto, sl);
+            const uint32_t acc = o.kind == ZP_B_ICMPV4 ? 0u : pseudo(o, v4, proto, sl);
             const uint32_t at = o.kind == ZP_B_TCP ? 16u : o.kind == ZP_B_UDP ? 6u : 2u;
             w8(v, hl + at, 0); w8(v, hl + at + 1, 0);                    // set_checksum
-            if (coop) wave_sync();
-            const uint16_t c = bcsum(v, hl, acc, coop, lane);
+            uint16_t c;
+            if (COOP) {
+                wave_sync();
+                c = bcsum_lds(stage, shift, hl, n, acc, lane);
+            } else {
+                c = bcsum_seq((const uint8_t*)v.b, hl, n, acc);
+            }
             w16(v, hl + at, c);
             hl += o.kind == ZP_B_TCP ? start : 8u;
             break;
@@ -366,10 +461,13 @@ __device__ int run_chain(BView& v, const zp_build_op* __restrict__ ops, uint32_t
         default:
             e = ZP_BERR_TRANSITION;
         }
-        if (e) { *hl_out = hl; *done_out = k; return e; }
+        const uint32_t top = base + ext < n ? base + ext : n;
+        hw = top > hw ? top : hw;
+        if (e) { *hl_out = hl; *done_out = k; *hw_out = hw; return e; }
     }
     *hl_out = hl;
     *done_out = nops;
+    *hw_out = hw;
     return 0;
 }
 
@@ -378,51 +476,61 @@ zp_build_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs,
                 const uint32_t* __restrict__ lens, uint64_t n, const zp_build_op* __restrict__ ops,
                 const uint32_t* __restrict__ op_start, const uint8_t* __restrict__ data,
                 zp_build_result* __restrict__ results) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds_all[ZB_WAVES][ZB_LDS];
-    const int lane = threadIdx.x & 63;
-    const int wid = threadIdx.x >> 6;
-    // wave-uniform frame index (scalar loads of its descriptors and ops)
-    const uint64_t i = (uint64_t)blockIdx.x * ZB_WAVES +
-                       (uint32_t)__builtin_amdgcn_readfirstlane(wid);
-    if (i >= n) return;
+    __shared__ __attribute__((aligned(16))) uint8_t lds_all[ZB_WAVES * ZB_F][ZB_LDS];
+    __shared__ __attribute__((aligned(16))) zp_build_op lds_ops[ZB_WAVES * ZB_F][ZB_OPS];
+    // A group of ZB_G lanes builds one frame; the groups of a wave run side
+    // by side (same instructions for same-shaped chains).
+    const int lane = threadIdx.x & (ZB_G - 1);
+    const int slot = threadIdx.x / ZB_G;
+    const uint64_t i = (uint64_t)blockIdx.x * ZB_WAVES * ZB_F + slot;
+    if (i >= n) return;                              // whole group
     const uint32_t len = lens[i];
     uint8_t* const g = arena + offs[i];
     const uint32_t o0 = op_start[i], o1 = op_start[i + 1];
     const uint32_t shift = (uint32_t)((uintptr_t)g & 15);
     const bool coop = len + shift <= ZB_LDS;
-    uint8_t* lds = lds_all[wid];
-    BView v;
-    v.n = len;
-    v.hw = 0;
+    uint8_t ZB_LDSP* lds = (uint8_t ZB_LDSP*)lds_all[slot];
     uint8_t* const a0 = (uint8_t*)((uintptr_t)g & ~(uintptr_t)15);
     const uint32_t nch = (len + shift + 15) >> 4;
-    if (coop) {
-        // stage the 16-B chunks holding the frame (bytes of neighbours in the
-        // edge chunks are staged but never written back)
-        for (uint32_t c = lane; c < nch; c += 64)
-            *(uint4*)(lds + 16 * c) = *(const uint4*)(a0 + 16 * c);
+    uint32_t hl = 0, done = 0, hw = 0;
+    int err = ZP_BERR_TRANSITION;
+    const uint32_t nops = o1 >= o0 ? o1 - o0 : 0u;
+    OpSrc src{(const zp_build_op ZB_LDSP*)lds_ops[slot], ops + o0};
+    {
+        // one round trip: the chain's first ops (4 lanes per 64-B op) and,
+        // in LDS mode, the 16-B chunks holding the frame (bytes of
+        // neighbours in the edge chunks are staged but never written back)
+        const uint32_t nq = 4 * (nops < ZB_OPS ? nops : ZB_OPS);
+        for (uint32_t q = lane; q < nq; q += ZB_G)
+            ((zb_u32x4 ZB_LDSP*)lds_ops[slot])[q] = ((const zb_u32x4*)(ops + o0))[q];
+        if (coop)
+            for (uint32_t c = lane; c < nch; c += ZB_G)
+                *(zb_u32x4 ZB_LDSP*)(lds + 16 * c) = *(const zb_u32x4*)(a0 + 16 * c);
         wave_sync();
-        v.b = lds + shift;
-    } else {
-        v.b = g;
     }
-    uint32_t hl = 0, done = 0;
-    const int err = o1 >= o0 ? run_chain(v, ops + o0, o1 - o0, data, coop, lane, &hl, &done)
-                             : ZP_BERR_TRANSITION;
-    if (coop && v.hw) {
-        wave_sync();
-        // write back frame bytes [0, hw): whole chunks as 16-B stores, the
-        // partial edge chunks byte by byte (never a neighbour's byte)
-        const uint32_t end = shift + v.hw;            // in staged coordinates
-        for (uint32_t c = lane; c < (end + 15) >> 4; c += 64) {
-            const uint32_t lo = 16 * c, hi = lo + 16;
-            if (lo >= shift && hi <= end) {
-                *(uint4*)(a0 + lo) = *(const uint4*)(lds + lo);
-            } else {
-                for (uint32_t q = lo < shift ? shift : lo; q < (hi < end ? hi : end); ++q)
-                    a0[q] = lds[q];
+    if (coop) {
+        BView<uint8_t ZB_LDSP*> v{lds + shift, len, true};
+        if (o1 >= o0)
+            err = run_chain<true>(v, lds, shift, src, nops, data, lane, &hl, &done, &hw);
+        if (hw) {
+            wave_sync();
+            // write back frame bytes [0, hw): whole chunks as 16-B stores, the
+            // partial edge chunks byte by byte (never a neighbour's byte)
+            const uint32_t end = shift + hw;          // in staged coordinates
+            for (uint32_t c = lane; c < (end + 15) >> 4; c += ZB_G) {
+                const uint32_t lo = 16 * c, hi = lo + 16;
+                if (lo >= shift && hi <= end) {
+                    *(zb_u32x4*)(a0 + lo) = *(const zb_u32x4 ZB_LDSP*)(lds + lo);
+                } else {
+                    for (uint32_t q = lo < shift ? shift : lo; q < (hi < end ? hi : end); ++q)
+                        a0[q] = lds[q];
+                }
             }
         }
+    } else {
+        BView<uint8_t*> v{g, len, true};
+        if (o1 >= o0)
+            err = run_chain<false>(v, lds, shift, src, nops, data, lane, &hl, &done, &hw);
     }
     if (results && lane == 0) {
         zp_build_result r;
@@ -443,7 +551,8 @@ extern "C" int zp_build_batch_device(uint8_t* arena, const uint64_t* offs, const
         snprintf(zp__errbuf(), 256, "zp_build_batch_device: null pointer");
         return -1;
     }
-    const uint64_t blocks = (n + ZB_WAVES - 1) / ZB_WAVES;
+    const uint64_t per_block = (uint64_t)ZB_WAVES * ZB_F;
+    const uint64_t blocks = (n + per_block - 1) / per_block;
     if (blocks > 0x7FFFFFFFull) {
         snprintf(zp__errbuf(), 256, "zp_build_batch_device: batch too large");
         return -1;
