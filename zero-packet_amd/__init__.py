@@ -11,7 +11,7 @@ Import with importlib (the directory name has a hyphen):
   zp.PacketParser.parse(frame)               one frame through the GPU path
   zp.PacketParser.from_record(frame, rec)    reference-shaped views over a record
 """
-from . import _lib, records, ring, shard  # noqa: F401
+from . import _lib, debugfmt, records, ring, shard  # noqa: F401
 from .parser import (ArpReader, AuthenticationHeaderReader, EthernetReader,  # noqa: F401
                      ExtensionHeaders, FragmentHeaderReader, Icmpv4Reader, Icmpv6Reader,
                      IpInIp, IPv4Reader, IPv6Reader, OptionsHeaderReader, PacketParser,

@@ -436,6 +436,11 @@ class PacketParser:
             p.icmpv6 = Icmpv6Reader(frame[l4:])
         return p
 
+    def debug(self, pretty=False):
+        """format!("{:?}") / format!("{:#?}") of the reference (debugfmt.py)."""
+        from .debugfmt import debug
+        return debug(self, pretty)
+
     @classmethod
     def parse(cls, frame):
         """PacketParser::parse (parser.rs:53) through the GPU path."""
