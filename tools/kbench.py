@@ -81,6 +81,18 @@ def main():
                 nbytes = buf.numel() // region * region
                 print(f"membw region={region >> 10}KiB G={g}: "
                       f"{nbytes / (np.median(ms) * 1e-3) / 1e9:.0f} GB/s", flush=True)
+        mb.membw_region2.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                     ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p]
+        names = {0: "1 wave/WG, G8", 1: "4 waves/WG, G8", 2: "4 waves interleaved, G8",
+                 3: "8 waves interleaved, G8", 4: "8 waves interleaved, G4",
+                 5: "1 wave/WG, G16"}
+        for region in (48 << 10, 96 << 10):
+            for mode, label in names.items():
+                ms = time_launches(lambda: mb.membw_region2(buf.data_ptr(), buf.numel(),
+                                                            rout.data_ptr(), region, mode, None), 10)
+                nbytes = buf.numel() // region * region
+                print(f"membw region2={region >> 10}KiB {label}: "
+                      f"{nbytes / (np.median(ms) * 1e-3) / 1e9:.0f} GB/s", flush=True)
         del buf, rout
         torch.cuda.empty_cache()
     for cfg in args.configs.split(","):

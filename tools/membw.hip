@@ -79,3 +79,73 @@ extern "C" int membw_region(const void* p, uint64_t bytes, uint32_t* out, uint64
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+
+// Variants of the region pattern (A/B for the parse kernel's decomposition):
+//   WAVES waves per workgroup; ILV = 1: wave w owns region w (as above);
+//   ILV = 1 with WAVES = 1: the parse kernel's one-wave workgroups;
+//   ILV = W: the W waves of a workgroup share W consecutive regions and
+//   interleave their 1 KiB items (wave w reads items q*W + w), so the
+//   resident waves read a denser band of memory.
+template <int G, int WAVES, bool ILV>
+__global__ void __launch_bounds__(64 * WAVES) read_region2(const uint8_t* __restrict__ p,
+                                                           uint64_t region, uint64_t nreg,
+                                                           uint32_t* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int wid = threadIdx.x >> 6;
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    uint64_t items, first, stride;
+    const uint8_t* base;
+    if (ILV) {
+        const uint64_t g0 = (uint64_t)blockIdx.x * WAVES;       // first region of the block
+        if (g0 >= nreg) return;
+        const uint64_t nr = nreg - g0 < WAVES ? nreg - g0 : WAVES;
+        base = p + g0 * region;
+        items = nr * region / 1024;
+        first = wid;
+        stride = WAVES;
+    } else {
+        const uint64_t w = (uint64_t)blockIdx.x * WAVES + wid;
+        if (w >= nreg) return;
+        base = p + w * region;
+        items = region / 1024;
+        first = 0;
+        stride = 1;
+    }
+    uint32_t acc = 0;
+    for (uint64_t i = first; i < items; i += G * stride) {
+        u32x4 v[G];
+#pragma unroll
+        for (int q = 0; q < G; ++q) {
+            uint64_t it = i + q * stride;
+            it = it < items ? it : items - 1;
+            v[q] = __builtin_nontemporal_load(
+                (const __attribute__((address_space(1))) u32x4*)(base + it * 1024 + lane * 16));
+        }
+#pragma unroll
+        for (int q = 0; q < G; ++q) acc += v[q].x ^ v[q].y ^ v[q].z ^ v[q].w;
+    }
+    out[((uint64_t)blockIdx.x * WAVES + wid) * 64 + lane] = acc;
+}
+
+extern "C" int membw_region2(const void* p, uint64_t bytes, uint32_t* out, uint64_t region,
+                             int mode, void* stream) {
+    const uint64_t nreg = bytes / region;
+    hipStream_t s = (hipStream_t)stream;
+    const uint8_t* q = (const uint8_t*)p;
+    switch (mode) {
+    case 0: hipLaunchKernelGGL((read_region2<8, 1, false>), dim3((unsigned)nreg), dim3(64), 0, s,
+                               q, region, nreg, out); break;
+    case 1: hipLaunchKernelGGL((read_region2<8, 4, false>), dim3((unsigned)((nreg + 3) / 4)),
+                               dim3(256), 0, s, q, region, nreg, out); break;
+    case 2: hipLaunchKernelGGL((read_region2<8, 4, true>), dim3((unsigned)((nreg + 3) / 4)),
+                               dim3(256), 0, s, q, region, nreg, out); break;
+    case 3: hipLaunchKernelGGL((read_region2<8, 8, true>), dim3((unsigned)((nreg + 7) / 8)),
+                               dim3(512), 0, s, q, region, nreg, out); break;
+    case 4: hipLaunchKernelGGL((read_region2<4, 8, true>), dim3((unsigned)((nreg + 7) / 8)),
+                               dim3(512), 0, s, q, region, nreg, out); break;
+    case 5: hipLaunchKernelGGL((read_region2<16, 1, false>), dim3((unsigned)nreg), dim3(64), 0, s,
+                               q, region, nreg, out); break;
+    default: return -1;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}

@@ -48,6 +48,9 @@
 #ifndef ZP_G
 #define ZP_G 8               // stream items (1 KiB loads) per group
 #endif
+#ifndef ZP_K
+#define ZP_K 1               // consecutive tiles per wave
+#endif
 // Timing-only ablations (tools/build_variants.sh); never set in the product:
 //   ZP_ABL_FAKE_WALK  replace the walk by "pending L4 at offset 42"
 //   ZP_ABL_STREAM_OFF skip the stream loads
@@ -839,36 +842,40 @@ zp_parse_kernel(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ 
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
     WaveLds& lds = lds_all[wid];
-    const uint64_t t = (uint64_t)blockIdx.x * ZP_WAVES + wid;
-    if (t * 64 >= n) return;                       // wave-uniform
-#ifdef ZP_STAMPS
-    const uint64_t wave_id = t;
-#endif
-    STAMP(0);
     const uintptr_t fallback = (uintptr_t)&zp_safe_chunk;   // dummy loads when T == 0
     uint4* win = &lds.win[0];
     uint4* tail = &lds.win[ZP_WIN_CH * 64];
-    uint32_t len;
-    uintptr_t ga;
-    load_desc(arena, offs, lens, n, t, lane, len, ga);
-    TileState s;
-    tile_setup(s, t, len, ga, n, lane, lds);
-    STAMP(1);
-    // stream: one group of ZP_G items per iteration (group 0 outside the loop,
-    // so no load is in flight across the loop back-edge)
-    uint4 va[ZP_G];
-    uint32_t ka[ZP_G];
-    issue_group<ZP_G>(0, s.nitems, s.cur, s.R, lane, fallback, va, ka);
-    STAMP(2);
-    consume_group<ZP_G>(0, s.nitems, lane, va, ka, win, tail, lds.cend, s.run);
-    for (uint32_t i0 = ZP_G; i0 < s.nitems; i0 += ZP_G) {
-        issue_group<ZP_G>(i0, s.nitems, s.cur, s.R, lane, fallback, va, ka);
-        consume_group<ZP_G>(i0, s.nitems, lane, va, ka, win, tail, lds.cend, s.run);
+    // ZP_K consecutive tiles per wave (one contiguous band of the arena)
+    for (uint32_t k = 0; k < ZP_K; ++k) {
+        const uint64_t t = ((uint64_t)blockIdx.x * ZP_WAVES + wid) * ZP_K + k;
+        if (t * 64 >= n) return;                   // wave-uniform
+#ifdef ZP_STAMPS
+        const uint64_t wave_id = t;
+#endif
+        STAMP(0);
+        if (k) wave_lds_fence();                   // previous tile's LDS reads done
+        uint32_t len;
+        uintptr_t ga;
+        load_desc(arena, offs, lens, n, t, lane, len, ga);
+        TileState s;
+        tile_setup(s, t, len, ga, n, lane, lds);
+        STAMP(1);
+        // stream: one group of ZP_G items per iteration (group 0 outside the
+        // loop, so no load is in flight across the loop back-edge)
+        uint4 va[ZP_G];
+        uint32_t ka[ZP_G];
+        issue_group<ZP_G>(0, s.nitems, s.cur, s.R, lane, fallback, va, ka);
+        STAMP(2);
+        consume_group<ZP_G>(0, s.nitems, lane, va, ka, win, tail, lds.cend, s.run);
+        for (uint32_t i0 = ZP_G; i0 < s.nitems; i0 += ZP_G) {
+            issue_group<ZP_G>(i0, s.nitems, s.cur, s.R, lane, fallback, va, ka);
+            consume_group<ZP_G>(i0, s.nitems, lane, va, ka, win, tail, lds.cend, s.run);
+        }
+        wave_lds_fence();                          // LDS written by other lanes
+        STAMP(3);
+        tile_finish(s, n, lane, lds, records, inner_ext);
+        STAMP(4);
     }
-    wave_lds_fence();                              // LDS written by other lanes
-    STAMP(3);
-    tile_finish(s, n, lane, lds, records, inner_ext);
-    STAMP(4);
 }
 
 extern "C" int zp_parse_batch_device(const uint8_t* arena, const uint64_t* offs,
@@ -880,7 +887,8 @@ extern "C" int zp_parse_batch_device(const uint8_t* arena, const uint64_t* offs,
         snprintf(g_last_error, sizeof g_last_error, "zp_parse_batch_device: null pointer");
         return -1;
     }
-    const uint64_t blocks = (n + 64 * ZP_WAVES - 1) / (64 * ZP_WAVES);
+    const uint64_t per_block = 64ull * ZP_WAVES * ZP_K;
+    const uint64_t blocks = (n + per_block - 1) / per_block;
     if (blocks > 0x7FFFFFFFull) {
         snprintf(g_last_error, sizeof g_last_error, "zp_parse_batch_device: batch too large");
         return -1;
