@@ -289,6 +289,14 @@ int zp_extract_columns_device(const uint8_t* arena, const uint64_t* offs,
                               const uint32_t* lens, const zp_record* records, uint64_t n,
                               void* const* cols, void* stream);
 
+/* zp_parse_batch_device and zp_extract_columns_device fused: one pass over
+ * the frames writes the records and the requested columns (read from the
+ * parse kernel's staged header window; cols as above, NULL entries skipped).
+ * Same results as the two calls in sequence. */
+int zp_parse_batch_columns_device(const uint8_t* arena, const uint64_t* offs,
+                                  const uint32_t* lens, uint64_t n, zp_record* records,
+                                  zp_ext_offsets* inner_ext, void* const* cols, void* stream);
+
 /* ------------------------------------------------------------------------- */
 /* Batched PacketBuilder. The reference builds one    */
 /* frame with a typestate chain over a caller-sized buffer                    */

@@ -40,6 +40,9 @@ def main():
     ap.add_argument("--membw", action="store_true")
     ap.add_argument("--no-base", action="store_true", help="time only --variants (PMC runs)")
     ap.add_argument("--columns", action="store_true", help="also time zp_extract_columns_device")
+    ap.add_argument("--c2cold", action="store_true",
+                    help="c2 (1M x 64 B = 64 MiB, fits the 256 MiB MALL) warm vs cold: "
+                         "8 rotating copies (512 MiB) so every launch reads from HBM")
     args = ap.parse_args()
     zp = importlib.import_module("zero-packet_amd")
     dev = torch.device("cuda:0")
@@ -95,7 +98,33 @@ def main():
                       f"{nbytes / (np.median(ms) * 1e-3) / 1e9:.0f} GB/s", flush=True)
         del buf, rout
         torch.cuda.empty_cache()
-    for cfg in args.configs.split(","):
+    if args.c2cold:
+        n = 1 << 20
+        copies = [zp.batch.generate("c2", n, device=dev) for _ in range(8)]
+        rec = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+        lib = zp._lib.hip()
+        nbytes = int(copies[0][2].to(torch.int64).sum())
+        for label, order in (("warm (same copy)", [0] * 8), ("cold (8 rotating copies)",
+                                                            list(range(8)))):
+            ms = []
+            for r in range(args.rounds):
+                s = torch.cuda.current_stream()
+                ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                      for _ in order]
+                for (a, b), k in zip(ev, order):
+                    ar, of, ln = copies[k]
+                    a.record(s)
+                    lib.zp_parse_batch_device(ar.data_ptr(), of.data_ptr(), ln.data_ptr(), n,
+                                              rec.data_ptr(), None, None)
+                    b.record(s)
+                torch.cuda.synchronize()
+                ms += [a.elapsed_time(b) for a, b in ev]
+            med = float(np.median(ms))
+            print(f"c2 {label}: {med * 1e3:8.1f} us  {nbytes / med / 1e6:7.0f} GB/s  "
+                  f"{n / med / 1e3:8.0f} Mpkt/s", flush=True)
+        del copies
+        torch.cuda.empty_cache()
+    for cfg in [c for c in args.configs.split(",") if c]:
         n = sizes[cfg]
         arena, offs, lens = zp.batch.generate(cfg, n, device=dev)
         rec = torch.empty((n, 32), dtype=torch.uint8, device=dev)
@@ -132,6 +161,13 @@ def main():
                 rbytes = n * (32 + 12 + 128)
                 print(f"{cfg} columns[{label}]: {med:8.3f} ms  write {wbytes / med / 1e6:6.0f} GB/s"
                       f"  (write+read {(wbytes + rbytes) / med / 1e6:6.0f} GB/s)  "
+                      f"{n / med / 1e3:8.0f} Mpkt/s", flush=True)
+                ms = time_launches(lambda: zp.columns.parse_with_columns(
+                    arena, offs, lens, names=names, records=rec, inner_ext=ext, out=out),
+                    args.reps * args.rounds)
+                med = float(np.median(ms))
+                print(f"{cfg} fused parse+columns[{label}]: {med:8.3f} ms  "
+                      f"{(nbytes + wbytes) / med / 1e6:6.0f} GB/s (frames + columns)  "
                       f"{n / med / 1e3:8.0f} Mpkt/s", flush=True)
                 del out
         del arena, offs, lens, rec, ext

@@ -69,3 +69,32 @@ def extract(arena, offs, lens, records, names=None, out=None, stream=None):
                                               records.data_ptr(), n, ptrs, s)
     _lib.check(rc, "zp_extract_columns_device")
     return {k: out[k] for k in names}
+
+
+def parse_with_columns(arena, offs, lens, names=None, records=None, inner_ext=None, out=None,
+                       stream=None):
+    """zp_parse_batch_columns_device: records and the requested columns in one
+    pass over the frames. Returns (records, inner_ext, {name: tensor})."""
+    for t in (arena, offs, lens):
+        if not t.is_cuda:
+            raise RuntimeError("columns.parse_with_columns needs device tensors (no CPU fallback)")
+    n = offs.numel()
+    d = arena.device
+    if records is None:
+        records = torch.empty((n, 32), dtype=torch.uint8, device=d)
+    if inner_ext is None:
+        inner_ext = torch.zeros((n, 12), dtype=torch.uint8, device=d)
+    names = list(names) if names is not None else NAMES
+    out = dict(out or {})
+    ptrs = (ctypes.c_void_p * len(COLUMNS))()
+    for name in names:
+        if name not in out:
+            out[name] = _alloc(name, n, d)
+        ptrs[INDEX[name]] = out[name].data_ptr()
+    s = ctypes.c_void_p(stream) if stream is not None else \
+        ctypes.c_void_p(torch.cuda.current_stream(d).cuda_stream)
+    rc = _lib.hip().zp_parse_batch_columns_device(arena.data_ptr(), offs.data_ptr(),
+                                                  lens.data_ptr(), n, records.data_ptr(),
+                                                  inner_ext.data_ptr(), ptrs, s)
+    _lib.check(rc, "zp_parse_batch_columns_device")
+    return records, inner_ext, {k: out[k] for k in names}

@@ -36,6 +36,7 @@
 
 #include "../../include/zero_packet.h"
 #include "../../include/zero_packet_errstr.h"
+#include "zp_cols.h"
 
 #ifndef ZP_WIN
 #define ZP_WIN 128           // LDS header window bytes per frame (multiple of 16)
@@ -756,10 +757,27 @@ __device__ __forceinline__ void wave_lds_fence() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Header walk + checksum verdict + record store of a streamed tile.
+// Byte reader over a FrameView for the fused column views (zp_cols.h): the
+// LDS window, then plain global byte loads (the walk's one-chunk cache here
+// makes the fused kernel spill to scratch).
+struct ViewReader {
+    const FrameView& f;
+    __device__ __forceinline__ uint32_t operator()(uint32_t x) {
+        if (x < f.wlen) {
+            const uint32_t y = x + f.shift;
+            return (win_dw(f, y >> 2) >> ((y & 3) * 8)) & 0xFFu;
+        }
+        return *(const ZP_GLOBAL uint8_t*)((uintptr_t)f.g + x);
+    }
+};
+
+// Header walk + checksum verdict + record store of a streamed tile; with COLS
+// also the column views, from the same LDS window (no second pass).
+template <bool COLS>
 __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, WaveLds& lds,
                                             zp_record* __restrict__ records,
-                                            zp_ext_offsets* __restrict__ inner_ext) {
+                                            zp_ext_offsets* __restrict__ inner_ext,
+                                            const ColPtrs& cols) {
     uint4* tail = &lds.win[ZP_WIN_CH * 64];
     const uint8_t* g = (const uint8_t*)s.ga;
     FrameView fv;
@@ -810,6 +828,10 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
     dst[0] = q2[0];
     dst[1] = q2[1];
     if (inner_ext && (rec.flags & ZP_F_INNER_EXT)) inner_ext[p] = w.inner;
+    if (COLS) {
+        ViewReader rdr{fv};
+        emit_columns(rdr, rec, rec.err == 0 && (rec.flags & ZP_F_ETHERNET), s.len, p, cols);
+    }
 }
 
 // Descriptor loads are unconditional (clamped index, masked after): a load
@@ -834,10 +856,13 @@ __device__ __forceinline__ void load_desc(const uint8_t* arena, const uint64_t* 
 #else
 #define ZP_KATTR __launch_bounds__(64 * ZP_WAVES)
 #endif
-__global__ void ZP_KATTR
-zp_parse_kernel(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs,
-                const uint32_t* __restrict__ lens, uint64_t n,
-                zp_record* __restrict__ records, zp_ext_offsets* __restrict__ inner_ext) {
+template <bool COLS>
+__device__ __forceinline__ void parse_tiles(const uint8_t* __restrict__ arena,
+                                            const uint64_t* __restrict__ offs,
+                                            const uint32_t* __restrict__ lens, uint64_t n,
+                                            zp_record* __restrict__ records,
+                                            zp_ext_offsets* __restrict__ inner_ext,
+                                            const ColPtrs& cols) {
     __shared__ WaveLds lds_all[ZP_WAVES];
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
@@ -873,9 +898,26 @@ zp_parse_kernel(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ 
         }
         wave_lds_fence();                          // LDS written by other lanes
         STAMP(3);
-        tile_finish(s, n, lane, lds, records, inner_ext);
+        tile_finish<COLS>(s, n, lane, lds, records, inner_ext, cols);
         STAMP(4);
     }
+}
+
+__global__ void ZP_KATTR
+zp_parse_kernel(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs,
+                const uint32_t* __restrict__ lens, uint64_t n,
+                zp_record* __restrict__ records, zp_ext_offsets* __restrict__ inner_ext) {
+    const ColPtrs none{};
+    parse_tiles<false>(arena, offs, lens, n, records, inner_ext, none);
+}
+
+// Parse + column views in one pass (zp_parse_batch_columns_device).
+__global__ void ZP_KATTR
+zp_parse_columns_kernel(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs,
+                        const uint32_t* __restrict__ lens, uint64_t n,
+                        zp_record* __restrict__ records, zp_ext_offsets* __restrict__ inner_ext,
+                        ColPtrs cols) {
+    parse_tiles<true>(arena, offs, lens, n, records, inner_ext, cols);
 }
 
 extern "C" int zp_parse_batch_device(const uint8_t* arena, const uint64_t* offs,
@@ -897,5 +939,29 @@ extern "C" int zp_parse_batch_device(const uint8_t* arena, const uint64_t* offs,
                        (hipStream_t)stream, arena, offs, lens, n, records, inner_ext);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) { set_err("zp_parse_kernel launch", e); return -2; }
+    return 0;
+}
+
+extern "C" int zp_parse_batch_columns_device(const uint8_t* arena, const uint64_t* offs,
+                                             const uint32_t* lens, uint64_t n,
+                                             zp_record* records, zp_ext_offsets* inner_ext,
+                                             void* const* cols, void* stream) {
+    if (n == 0) return 0;
+    if (!arena || !offs || !lens || !records || !cols) {
+        snprintf(g_last_error, sizeof g_last_error, "zp_parse_batch_columns_device: null pointer");
+        return -1;
+    }
+    ColPtrs c;
+    for (int k = 0; k < ZP_COL_COUNT; ++k) c.p[k] = (uint8_t*)cols[k];
+    const uint64_t per_block = 64ull * ZP_WAVES * ZP_K;
+    const uint64_t blocks = (n + per_block - 1) / per_block;
+    if (blocks > 0x7FFFFFFFull) {
+        snprintf(g_last_error, sizeof g_last_error, "zp_parse_batch_columns_device: batch too large");
+        return -1;
+    }
+    hipLaunchKernelGGL(zp_parse_columns_kernel, dim3((unsigned)blocks), dim3(64 * ZP_WAVES), 0,
+                       (hipStream_t)stream, arena, offs, lens, n, records, inner_ext, c);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) { set_err("zp_parse_columns_kernel launch", e); return -2; }
     return 0;
 }
