@@ -618,18 +618,42 @@ __device__ __forceinline__ void issue_group(uint32_t i0, uint32_t nitems, Cursor
                                             const Ranked& R, int lane, uintptr_t fallback,
                                             uint4 (&v)[G], uint32_t (&keep)[G]) {
     uintptr_t a[G];
+#ifndef ZP_FMASK_ITEM
+    // The G items' frame-start masks in one LDS round trip (G divides 64, so
+    // the group never straddles a rebuild of the mask table).
+    static_assert(64 % G == 0 && G % 2 == 0, "group size must be even and divide 64");
+    if ((i0 & 63u) == 0 && i0 < nitems) build_starts(i0, c, R, lane);   // wave-uniform
+    // G/2 ds_read_b128 issued back to back, then one wait
+    uint64_t Fq[G];
+    zp_u32x4 m[G / 2];
+    const zp_u32x4* sp = (const zp_u32x4*)&c.starts[i0 & 63u];
+#pragma unroll
+    for (int q = 0; q < G / 2; ++q) m[q] = sp[q];
+#pragma unroll
+    for (int q = 0; q < G; ++q) {
+        const uint32_t lo = (q & 1) ? m[q / 2].z : m[q / 2].x;
+        const uint32_t hi = (q & 1) ? m[q / 2].w : m[q / 2].y;
+        // (readfirstlane returns int: cast before widening, no sign extension)
+        const uint64_t fu = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(hi) << 32) |
+                            (uint32_t)__builtin_amdgcn_readfirstlane(lo);
+        Fq[q] = i0 + q < nitems ? fu : 0ull;
+    }
+#endif
 #pragma unroll
     for (int q = 0; q < G; ++q) {
         const uint32_t i = i0 + q;
         const uint32_t base = 64u * i;
+#ifdef ZP_FMASK_ITEM
         if ((i & 63u) == 0 && i < nitems) build_starts(i, c, R, lane);   // wave-uniform
         uint64_t F = 0;
         if (i < nitems) {
             const uint64_t f = c.starts[i & 63u];
-            // (readfirstlane returns int: cast before widening, no sign extension)
             F = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(f >> 32)) << 32) |
                 (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)f);
         }
+#else
+        const uint64_t F = Fq[q];
+#endif
         const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(F >> 32),
                                    __builtin_amdgcn_mbcnt_lo((uint32_t)F, 0u));
         uint32_t r = c.rbase + below + (uint32_t)((F >> lane) & 1u);
