@@ -417,6 +417,14 @@ int zp_build_batch_device(uint8_t* arena, const uint64_t* offs, const uint32_t* 
                           uint64_t n, const zp_build_op* ops, const uint32_t* op_start,
                           const uint8_t* data, zp_build_result* results, void* stream);
 
+/* The same over host buffers (a transmit ring), through `ctx`: the frames'
+ * bytes go H2D, the chains run, the frame bytes come back. data_bytes is the
+ * size of the data blob. Synchronous. Returns 0 or negative on failure. */
+int zp_build_batch_host(zp_ctx* ctx, uint8_t* arena, uint64_t arena_bytes,
+                        const uint64_t* offs, const uint32_t* lens, uint64_t n,
+                        const zp_build_op* ops, const uint32_t* op_start,
+                        const uint8_t* data, uint64_t data_bytes, zp_build_result* results);
+
 /* ------------------------------------------------------------------------- */
 /* Synthetic batch generator (BASELINE.json configs 1-5), built from the      */
 /* builder's checksum-fill semantics (builder.rs:473-474,515-516,553,592-593).*/

@@ -20,10 +20,13 @@
 #include <array>
 #include <cstddef>
 #include <cstdint>
+#include <cstring>
 #include <optional>
 #include <stdexcept>
 #include <string>
+#include <type_traits>
 #include <utility>
+#include <vector>
 
 #include "zero_packet.h"
 #include "zero_packet_errstr.h"
@@ -436,6 +439,250 @@ inline void parse_batch_device(const uint8_t* arena, const uint64_t* offs, const
     if (zp_parse_batch_device(arena, offs, lens, n, records, inner_ext, stream) < 0)
         throw std::runtime_error(std::string("zp_parse_batch_device: ") + zp_last_error());
 }
+
+
+// ---------------------------------------------------------------------------
+// Host-ring ingestion: RAII over zp_ring_*.
+// ---------------------------------------------------------------------------
+class Ring {
+public:
+    Ring(int device, uint32_t nslots, uint64_t slot_bytes, uint64_t slot_frames)
+        : r_(zp_ring_create(device, nslots, slot_bytes, slot_frames)) {
+        if (!r_) throw std::runtime_error(std::string("zp_ring_create: ") + zp_last_error());
+    }
+    ~Ring() { zp_ring_destroy(r_); }
+    Ring(const Ring&) = delete;
+    Ring& operator=(const Ring&) = delete;
+    // The next FREE slot (pinned host views), or std::nullopt on timeout.
+    std::optional<zp_ring_slot> acquire(int64_t timeout_ms = -1) {
+        zp_ring_slot s{};
+        const int rc = zp_ring_acquire(r_, &s, timeout_ms);
+        if (rc == ZP_RING_TIMEOUT) return std::nullopt;
+        check(rc, "zp_ring_acquire");
+        return s;
+    }
+    void submit(const zp_ring_slot& s, uint64_t n) { check(zp_ring_submit(r_, s.id, n), "zp_ring_submit"); }
+    // The oldest submitted slot with its records, or std::nullopt on timeout.
+    std::optional<zp_ring_slot> wait(int64_t timeout_ms = -1) {
+        zp_ring_slot s{};
+        const int rc = zp_ring_wait(r_, &s, timeout_ms);
+        if (rc == ZP_RING_TIMEOUT) return std::nullopt;
+        check(rc, "zp_ring_wait");
+        return s;
+    }
+    void release(const zp_ring_slot& s) { check(zp_ring_release(r_, s.id), "zp_ring_release"); }
+
+private:
+    static void check(int rc, const char* what) {
+        if (rc < 0) throw std::runtime_error(std::string(what) + ": " + zp_last_error());
+    }
+    zp_ring* r_;
+};
+
+// ---------------------------------------------------------------------------
+// Batched PacketBuilder. Mirrors builder.rs:55-909:
+// the same method names and argument order, and the typestate graph of
+// builder.rs:817-909 is checked at compile time (a method a state does not
+// have fails a static_assert, as the Rust chain fails to compile). The chain
+// is recorded and runs on the GPU at build(), which throws zp::BuildError
+// with the reference's message when a step returns Err.
+// ---------------------------------------------------------------------------
+class BuildError : public std::runtime_error {
+public:
+    BuildError(int code, size_t header_len)
+        : std::runtime_error(zp_build_err_str(code) ? zp_build_err_str(code) : "build error"),
+          code_(code), header_len_(header_len) {}
+    int code() const { return code_; }
+    size_t header_len() const { return header_len_; }
+private:
+    int code_;
+    size_t header_len_;
+};
+
+namespace bstate {   // builder.rs:29-45
+enum S { Raw, Eth, Arp, V4, V6, Hbh, D1, Rt, Fr, Ah, D2, V4e, V6e, L4, Bad };
+constexpr int next(int st, int k) {
+    const bool l4v4 = k == ZP_B_TCP || k == ZP_B_UDP || k == ZP_B_ICMPV4;
+    const bool l4v6 = k == ZP_B_TCP || k == ZP_B_UDP || k == ZP_B_ICMPV6;
+    if (st == Raw) return (k >= ZP_B_ETHERNET && k <= ZP_B_ETHERNET_QINQ) ? Eth : Bad;
+    if (st == Eth) return k == ZP_B_ARP ? Arp : k == ZP_B_IPV4 ? V4 : k == ZP_B_IPV6 ? V6 : Bad;
+    if (st == V4) return l4v4 ? L4 : k == ZP_B_IPV4 ? V4e : k == ZP_B_IPV6 ? V6e : Bad;
+    if (st == V4e) return l4v4 ? L4 : Bad;
+    if (st == V6e) return l4v6 ? L4 : Bad;
+    if (st >= V6 && st <= D2) {
+        if (l4v6) return L4;
+        if (k == ZP_B_IPV4) return V4e;
+        if (k == ZP_B_IPV6) return V6e;
+        const int e = k == ZP_B_HOP_BY_HOP ? 0 : k == ZP_B_DEST_OPTS1 ? 1 : k == ZP_B_ROUTING ? 2
+                    : k == ZP_B_FRAGMENT ? 3 : k == ZP_B_AUTH ? 4 : k == ZP_B_DEST_OPTS2 ? 5 : -1;
+        const int succ[7] = {0x3F, 0x3E, 0x04, 0x38, 0x30, 0x20, 0x00};
+        return (e >= 0 && ((succ[st - V6] >> e) & 1)) ? Hbh + e : Bad;
+    }
+    return Bad;
+}
+}  // namespace bstate
+
+template <int S = bstate::Raw>
+class PacketBuilder {
+public:
+    // PacketBuilder::new (builder.rs:98): the caller's buffer, built in place.
+    PacketBuilder(uint8_t* bytes, size_t len) : bytes_(bytes), len_(len) {}
+
+    // The address type of tcp/udp: &[u8; 4] under IPv4 states, else &[u8; 16].
+    using Addr = std::conditional_t<S == bstate::V4 || S == bstate::V4e,
+                                    std::array<uint8_t, 4>, std::array<uint8_t, 16>>;
+    using Mac = std::array<uint8_t, 6>;
+    using Ip4 = std::array<uint8_t, 4>;
+    using Ip6 = std::array<uint8_t, 16>;
+
+    auto ethernet(const Mac& src_mac, const Mac& dest_mac, uint16_t ethertype) {
+        return push<ZP_B_ETHERNET>([&](zp_build_op& o) {
+            cp(o.src, src_mac); cp(o.dst, dest_mac); o.h[0] = ethertype; });
+    }
+    auto ethernet_vlan(const Mac& src_mac, const Mac& dest_mac, uint16_t ethertype, uint16_t tci) {
+        return push<ZP_B_ETHERNET_VLAN>([&](zp_build_op& o) {
+            cp(o.src, src_mac); cp(o.dst, dest_mac); o.h[0] = ethertype; o.h[1] = tci; });
+    }
+    auto ethernet_qinq(const Mac& src_mac, const Mac& dest_mac, uint16_t ethertype, uint16_t tci1,
+                       uint16_t tci2) {
+        return push<ZP_B_ETHERNET_QINQ>([&](zp_build_op& o) {
+            cp(o.src, src_mac); cp(o.dst, dest_mac);
+            o.h[0] = ethertype; o.h[1] = tci1; o.h[2] = tci2; });
+    }
+    auto arp(uint16_t hardware_type, uint16_t protocol_type, uint8_t hardware_address_length,
+             uint8_t protocol_address_length, uint16_t operation, const Mac& src_mac,
+             const Ip4& src_ip, const Mac& dest_mac, const Ip4& dest_ip) {
+        return push<ZP_B_ARP>([&](zp_build_op& o) {
+            o.h[0] = hardware_type; o.h[1] = protocol_type; o.h[2] = operation;
+            o.b[0] = hardware_address_length; o.b[1] = protocol_address_length;
+            cp(o.src, src_mac); cp(o.src + 6, src_ip); cp(o.dst, dest_mac); cp(o.dst + 6, dest_ip); });
+    }
+    auto ipv4(uint8_t version, uint8_t ihl, uint8_t dscp, uint8_t ecn, uint16_t total_length,
+              uint16_t identification, uint8_t flags, uint16_t fragment_offset, uint8_t ttl,
+              uint8_t protocol, const Ip4& src_ip, const Ip4& dest_ip) {
+        return push<ZP_B_IPV4>([&](zp_build_op& o) {
+            o.b[0] = version; o.b[1] = ihl; o.b[2] = dscp; o.b[3] = ecn; o.b[4] = flags;
+            o.b[5] = ttl; o.b[6] = protocol; o.h[0] = total_length; o.h[1] = identification;
+            o.h[2] = fragment_offset; cp(o.src, src_ip); cp(o.dst, dest_ip); });
+    }
+    auto ipv6(uint8_t version, uint8_t traffic_class, uint32_t flow_label, uint16_t payload_length,
+              uint8_t next_header, uint8_t hop_limit, const Ip6& src_addr, const Ip6& dest_addr) {
+        return push<ZP_B_IPV6>([&](zp_build_op& o) {
+            o.b[0] = version; o.b[1] = traffic_class; o.b[2] = next_header; o.b[3] = hop_limit;
+            o.w[0] = flow_label; o.h[0] = payload_length; cp(o.src, src_addr); cp(o.dst, dest_addr); });
+    }
+    auto hop_by_hop(uint8_t next_header, uint8_t extension_len, Bytes options) {
+        return push<ZP_B_HOP_BY_HOP>([&](zp_build_op& o) {
+            o.b[0] = next_header; o.b[1] = extension_len; blob(o, options); });
+    }
+    auto destination_options1(uint8_t next_header, uint8_t extension_len, Bytes options) {
+        return push<ZP_B_DEST_OPTS1>([&](zp_build_op& o) {
+            o.b[0] = next_header; o.b[1] = extension_len; blob(o, options); });
+    }
+    auto routing_header(uint8_t next_header, uint8_t header_ext_len, uint8_t routing_type,
+                        uint8_t segments_left, Bytes data) {
+        return push<ZP_B_ROUTING>([&](zp_build_op& o) {
+            o.b[0] = next_header; o.b[1] = header_ext_len; o.b[2] = routing_type;
+            o.b[3] = segments_left; blob(o, data); });
+    }
+    auto fragment_header(uint8_t next_header, uint16_t fragment_offset, bool m_flag,
+                         uint32_t identification) {
+        return push<ZP_B_FRAGMENT>([&](zp_build_op& o) {
+            o.b[0] = next_header; o.h[0] = fragment_offset; o.b[1] = m_flag ? 1 : 0;
+            o.w[0] = identification; });
+    }
+    auto authentication_header(uint8_t next_header, uint8_t payload_len, uint32_t spi,
+                               uint32_t seq_num, Bytes auth_data) {
+        return push<ZP_B_AUTH>([&](zp_build_op& o) {
+            o.b[0] = next_header; o.b[1] = payload_len; o.w[0] = spi; o.w[1] = seq_num;
+            blob(o, auth_data); });
+    }
+    auto destination_options2(uint8_t next_header, uint8_t extension_len, Bytes options) {
+        return push<ZP_B_DEST_OPTS2>([&](zp_build_op& o) {
+            o.b[0] = next_header; o.b[1] = extension_len; blob(o, options); });
+    }
+    auto tcp(const Addr& src_ip, uint16_t src_port, const Addr& dest_ip, uint16_t dest_port,
+             uint32_t sequence_number, uint32_t acknowledgment_number, uint8_t data_offset,
+             uint8_t reserved, uint8_t flags, uint16_t window_size, uint16_t urgent_pointer,
+             std::optional<Bytes> payload = std::nullopt) {
+        return push<ZP_B_TCP>([&](zp_build_op& o) {
+            cp(o.src, src_ip); cp(o.dst, dest_ip); o.h[0] = src_port; o.h[1] = dest_port;
+            o.w[0] = sequence_number; o.w[1] = acknowledgment_number; o.b[0] = data_offset;
+            o.b[1] = reserved; o.b[2] = flags; o.h[2] = window_size; o.h[3] = urgent_pointer;
+            opt_blob(o, payload); });
+    }
+    auto udp(const Addr& src_addr, uint16_t src_port, const Addr& dest_addr, uint16_t dest_port,
+             uint16_t length, std::optional<Bytes> payload = std::nullopt) {
+        return push<ZP_B_UDP>([&](zp_build_op& o) {
+            cp(o.src, src_addr); cp(o.dst, dest_addr); o.h[0] = src_port; o.h[1] = dest_port;
+            o.h[2] = length; opt_blob(o, payload); });
+    }
+    auto icmpv4(uint8_t icmp_type, uint8_t icmp_code, std::optional<Bytes> payload = std::nullopt) {
+        return push<ZP_B_ICMPV4>([&](zp_build_op& o) {
+            o.b[0] = icmp_type; o.b[1] = icmp_code; opt_blob(o, payload); });
+    }
+    auto icmpv6(const Ip6& src_addr, const Ip6& dest_addr, uint8_t icmp_type, uint8_t icmp_code,
+                std::optional<Bytes> payload = std::nullopt) {
+        return push<ZP_B_ICMPV6>([&](zp_build_op& o) {
+            cp(o.src, src_addr); cp(o.dst, dest_addr); o.b[0] = icmp_type; o.b[1] = icmp_code;
+            opt_blob(o, payload); });
+    }
+
+    // PacketBuilder::build (builder.rs:87): runs the chain on the GPU through
+    // ctx and returns the buffer. Throws BuildError on a step's Err.
+    Bytes build(zp_ctx* ctx) {
+        const uint64_t off = 0;
+        const uint32_t n = (uint32_t)len_;
+        const uint32_t start[2] = {0, (uint32_t)ops_.size()};
+        zp_build_result r{};
+        const int rc = zp_build_batch_host(ctx, bytes_, len_, &off, &n, 1,
+                                           ops_.empty() ? nullptr : ops_.data(), start,
+                                           data_.empty() ? nullptr : data_.data(), data_.size(), &r);
+        if (rc < 0) throw std::runtime_error(std::string("zp_build_batch_host: ") + zp_last_error());
+        header_len_ = r.header_len;
+        if (r.err) throw BuildError(r.err, r.header_len);
+        return Bytes{bytes_, len_};
+    }
+    // builder.rs:65-84, valid after build()
+    size_t header_len() const { return header_len_; }
+    size_t payload_len() const { return len_ - header_len_; }
+    Bytes payload() const { return Bytes{bytes_ + header_len_, len_ - header_len_}; }
+
+    const std::vector<zp_build_op>& ops() const { return ops_; }
+    const std::vector<uint8_t>& data() const { return data_; }
+
+private:
+    template <int> friend class PacketBuilder;
+    template <size_t N>
+    static void cp(uint8_t* d, const std::array<uint8_t, N>& a) { std::memcpy(d, a.data(), N); }
+    void blob(zp_build_op& o, Bytes b) {
+        o.data_off = (uint32_t)data_.size();
+        o.data_len = (uint32_t)b.len;
+        data_.insert(data_.end(), b.ptr, b.ptr + b.len);
+    }
+    void opt_blob(zp_build_op& o, const std::optional<Bytes>& b) {
+        if (b) blob(o, *b);
+        else { o.data_off = 0; o.data_len = ZP_BUILD_NO_DATA; }
+    }
+    template <int K, class F>
+    PacketBuilder<bstate::next(S, K)> push(F&& fill) {
+        static_assert(bstate::next(S, K) != bstate::Bad,
+                      "this PacketBuilder state has no such method (builder.rs:817-909)");
+        zp_build_op o{};
+        o.kind = (uint8_t)K;
+        fill(o);
+        ops_.push_back(o);
+        PacketBuilder<bstate::next(S, K)> nb(bytes_, len_);
+        nb.ops_ = std::move(ops_);
+        nb.data_ = std::move(data_);
+        return nb;
+    }
+    uint8_t* bytes_;
+    size_t len_;
+    size_t header_len_ = 0;
+    std::vector<zp_build_op> ops_;
+    std::vector<uint8_t> data_;
+};
 
 }  // namespace zp
 

@@ -139,3 +139,58 @@ def test_cpp_facade_parse_on_gpu(zp, golden):
     assert len(out) == len(exp)
     for got, (f, _, _, want) in zip(out, exp):
         assert got == want, (f.hex()[:64], got, want)
+
+
+# ---- §8(f) rows through the C++ facade: zp::PacketBuilder, zp::Ring -------
+
+BUILDER_SRC = os.path.join(ROOT, "tests", "cpp", "builder_main.cpp")
+
+
+def _compile_snippet(body, tmp_path):
+    src = tmp_path / "snippet.cpp"
+    src.write_text('#include "zero_packet.hpp"\nint main() {\n  uint8_t buf[128] = {0};\n'
+                   '  std::array<uint8_t, 6> m{};\n  std::array<uint8_t, 4> a{};\n'
+                   '  std::array<uint8_t, 16> a6{};\n  (void)a; (void)a6;\n'
+                   f"  auto b = zp::PacketBuilder<>(buf, 128){body};\n  (void)b;\n}}\n")
+    return subprocess.run(["g++", "-std=c++17", "-fsyntax-only", "-I", os.path.join(ROOT, "include"),
+                           str(src)], capture_output=True, text=True)
+
+
+@pytest.mark.parametrize("body,ok", [
+    (".ethernet(m, m, 2048).ipv4(4, 5, 0, 0, 50, 0, 0, 0, 64, 17, a, a).udp(a, 1, a, 2, 30)", True),
+    (".ethernet(m, m, 34525).ipv6(6, 0, 0, 0, 0, 64, a6, a6).hop_by_hop(0, 1, zp::Bytes{})"
+     ".routing_header(0, 1, 0, 0, zp::Bytes{}).ipv4(4, 5, 0, 0, 0, 0, 0, 0, 1, 6, a, a)"
+     ".tcp(a, 1, a, 2, 3, 4, 5, 0, 2, 9, 0)", True),
+    (".ethernet(m, m, 2048).tcp(a, 1, a, 2, 3, 4, 5, 0, 2, 9, 0)", False),          # no L3
+    (".ethernet(m, m, 34525).ipv6(6, 0, 0, 0, 0, 64, a6, a6)"
+     ".destination_options1(0, 1, zp::Bytes{}).fragment_header(0, 0, false, 0)", False),
+    (".ethernet(m, m, 2048).ipv4(4, 5, 0, 0, 0, 0, 0, 0, 1, 58, a, a).icmpv6(a6, a6, 1, 0)", False),
+    (".ethernet(m, m, 2048).ipv4(4, 5, 0, 0, 0, 0, 0, 0, 1, 6, a, a).tcp(a6, 1, a6, 2, 3, 4, 5, 0, 2, 9, 0)",
+     False),                                                                         # &[u8; 4] state
+])
+def test_cpp_builder_typestate(body, ok, tmp_path):
+    """The typestate graph of builder.rs:817-909 is enforced at compile time,
+    as in the Rust builder (CPU: g++ -fsyntax-only)."""
+    r = _compile_snippet(body, tmp_path)
+    assert (r.returncode == 0) == ok, r.stderr[-2000:]
+    if not ok and "static assertion" in r.stderr:
+        assert "builder.rs:817-909" in r.stderr
+
+
+@pytest.mark.gpu
+def test_cpp_builder_and_ring(zp, golden):
+    """builder.rs's own tests through zp::PacketBuilder (GPU build, GPU parse
+    back) and a zp::Ring round trip."""
+    os.makedirs(OUT, exist_ok=True)
+    exe = os.path.join(OUT, "builder_gpu")
+    lib = os.path.join(ROOT, "zero-packet_amd")
+    subprocess.run(["g++", "-std=c++17", "-O1", "-Wall", "-Wextra", "-Werror", "-I",
+                    os.path.join(ROOT, "include"), "-o", exe, BUILDER_SRC, "-L" + lib, "-lzp_hip",
+                    "-Wl,-rpath," + lib], check=True)
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0 and "ALL OK" in out.stdout, out.stdout[-3000:] + out.stderr[-2000:]
+    got = dict(l.split(" ", 1) for l in out.stdout.splitlines() if not l.startswith(("OK", "ALL")))
+    for v in golden["builder_vectors"]:
+        assert got[v["name"]] == v["bytes"], v["name"]
+    fx = {f["name"]: f["bytes"] for f in golden["fixtures"]}
+    assert got["build_parse_very_complex_packet"] == fx["build_parse_very_complex_packet"]

@@ -308,3 +308,100 @@ extern "C" int zp_parse_batch_host_multi(zp_ctx* const* ctxs, int nctx, const ui
     free(jobs); free(th); free(started);
     return rc;
 }
+
+// Batched PacketBuilder over host buffers (the builder's `&mut [u8]` in host
+// memory, e.g. a transmit ring): frames are cut into chunks whose byte span
+// fits the context's device arena; per chunk the frames' current bytes go
+// H2D (the writers read-modify-write them), the chains run
+// (zp_build_batch_device), and the span comes back D2H. The ops and the data
+// blob go H2D once. Synchronous.
+extern "C" int zp_build_batch_device(uint8_t*, const uint64_t*, const uint32_t*, uint64_t,
+                                     const zp_build_op*, const uint32_t*, const uint8_t*,
+                                     zp_build_result*, void*);
+
+extern "C" int zp_build_batch_host(zp_ctx* c, uint8_t* arena, uint64_t arena_bytes,
+                                   const uint64_t* offs, const uint32_t* lens, uint64_t n,
+                                   const zp_build_op* ops, const uint32_t* op_start,
+                                   const uint8_t* data, uint64_t data_bytes,
+                                   zp_build_result* results) {
+    if (!c || (n && (!arena || !offs || !lens || !ops || !op_start))) return -1;
+    if (n == 0) return 0;
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    if (hipSetDevice(c->device) != hipSuccess) return -2;
+    int rc = 0;
+    zp_build_op* d_ops = NULL;
+    uint32_t* d_start = NULL;
+    uint8_t* d_data = NULL;
+    zp_build_result* d_res = NULL;
+    uint32_t* h_start = NULL;
+    const uint64_t nops = op_start[n] - op_start[0];
+    hipStream_t s = c->s[0];
+    hipError_t e = hipMalloc(&d_ops, (nops ? nops : 1) * sizeof(zp_build_op));
+    if (e == hipSuccess) e = hipMalloc(&d_start, (c->chunk_pkts + 1) * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc(&d_data, data_bytes ? data_bytes : 16);
+    if (e == hipSuccess) e = hipMalloc(&d_res, c->chunk_pkts * sizeof(zp_build_result));
+    if (e == hipSuccess) e = hipHostMalloc(&h_start, (c->chunk_pkts + 1) * sizeof(uint32_t),
+                                           hipHostMallocDefault);
+    if (e == hipSuccess && nops)
+        e = hipMemcpyAsync(d_ops, ops + op_start[0], nops * sizeof(zp_build_op),
+                           hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && data_bytes)
+        e = hipMemcpyAsync(d_data, data, data_bytes, hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) {
+        snprintf(g_ctx_error, ERRBUF_LEN, "zp_build_batch_host setup: %s", hipGetErrorString(e));
+        rc = -2;
+    }
+    uint64_t i = 0;
+    while (rc == 0 && i < n) {
+        uint64_t lo = offs[i], hi = offs[i] + lens[i];
+        if (hi - lo > c->chunk_bytes || (arena_bytes && hi > arena_bytes)) {
+            snprintf(g_ctx_error, ERRBUF_LEN, "frame %llu does not fit the context chunk / arena",
+                     (unsigned long long)i);
+            rc = -3;
+            break;
+        }
+        uint64_t j = i + 1;
+        while (j < n && j - i < c->chunk_pkts) {
+            const uint64_t l2 = offs[j] < lo ? offs[j] : lo;
+            const uint64_t h2 = offs[j] + lens[j] > hi ? offs[j] + lens[j] : hi;
+            if (h2 - l2 > c->chunk_bytes || (arena_bytes && h2 > arena_bytes)) break;
+            lo = l2; hi = h2; ++j;
+        }
+        const uint64_t m = j - i;
+        for (uint64_t q = 0; q < m; ++q) {
+            c->h_offs[0][q] = offs[i + q] - lo;
+            c->h_lens[0][q] = lens[i + q];
+        }
+        for (uint64_t q = 0; q <= m; ++q) h_start[q] = op_start[i + q] - op_start[i];
+        memcpy(c->h_arena[0], arena + lo, hi - lo);
+        e = hipMemcpyAsync(c->d_arena[0], c->h_arena[0], hi - lo, hipMemcpyHostToDevice, s);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(c->d_offs[0], c->h_offs[0], m * 8, hipMemcpyHostToDevice, s);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(c->d_lens[0], c->h_lens[0], m * 4, hipMemcpyHostToDevice, s);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(d_start, h_start, (m + 1) * 4, hipMemcpyHostToDevice, s);
+        if (e != hipSuccess) { rc = -2; break; }
+        rc = zp_build_batch_device(c->d_arena[0], c->d_offs[0], c->d_lens[0], m,
+                                   d_ops + (op_start[i] - op_start[0]), d_start, d_data, d_res, s);
+        if (rc) break;
+        e = hipMemcpyAsync(c->h_arena[0], c->d_arena[0], hi - lo, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess && results)
+            e = hipMemcpyAsync(results + i, d_res, m * sizeof(zp_build_result),
+                               hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) { rc = -2; break; }
+        // frame bytes only: the chunk span may also cover bytes between frames
+        for (uint64_t q = 0; q < m; ++q)
+            memcpy(arena + offs[i + q], c->h_arena[0] + (offs[i + q] - lo), lens[i + q]);
+        i = j;
+    }
+    if (rc == -2 && e != hipSuccess)
+        snprintf(g_ctx_error, ERRBUF_LEN, "zp_build_batch_host: %s", hipGetErrorString(e));
+    (void)hipStreamSynchronize(s);
+    (void)hipFree(d_ops); (void)hipFree(d_start); (void)hipFree(d_data); (void)hipFree(d_res);
+    (void)hipHostFree(h_start);
+    (void)hipSetDevice(prev);
+    return rc;
+}

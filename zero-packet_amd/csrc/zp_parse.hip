@@ -42,6 +42,9 @@
 #define ZP_WIN 128           // LDS header window bytes per frame (multiple of 16)
 #endif
 #define ZP_WIN_CH (ZP_WIN / 16)
+// The window cell index (chunk * 64 + rank) travels in 9 bits of the item
+// descriptor (KEEP_WIN): at most 8 chunks.
+static_assert(ZP_WIN % 16 == 0 && ZP_WIN <= 128, "ZP_WIN must be a multiple of 16, <= 128");
 #define ZP_GIANT 65536u      // frames longer than this take the exact path
 #ifndef ZP_WAVES
 #define ZP_WAVES 1           // waves per workgroup (independent waves; 1 = finest LDS granularity)
