@@ -34,8 +34,11 @@ extern "C" char* zp__errbuf(void);
 #endif
 #define ZB_LDS (ZB_CAP + 32)   // + the frame's offset in its first 16-B chunk
 #ifndef ZB_OPS
-#define ZB_OPS 8               // ops of a chain prefetched to LDS (longer chains read the rest)
+#define ZB_OPS 4               // ops of a chain prefetched to LDS (longer chains read the rest)
 #endif
+#ifndef ZB_WPE
+#define ZB_WPE 5               // waves per SIMD: 96 VGPRs, 29 KB LDS per workgroup (measured 10 %
+#endif                         // faster than 4 waves with 8 prefetched ops)
 #ifndef ZB_G
 #define ZB_G 16                // lanes per frame: a wave builds 64 / ZB_G frames side by side
 #endif
@@ -471,7 +474,8 @@ __device__ int run_chain(BView<P>& v, const uint8_t ZB_LDSP* stage, uint32_t shi
     return 0;
 }
 
-__global__ void __launch_bounds__(64 * ZB_WAVES)
+#define ZB_KATTR __launch_bounds__(64 * ZB_WAVES) __attribute__((amdgpu_waves_per_eu(ZB_WPE)))
+__global__ void ZB_KATTR
 zp_build_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs,
                 const uint32_t* __restrict__ lens, uint64_t n, const zp_build_op* __restrict__ ops,
                 const uint32_t* __restrict__ op_start, const uint8_t* __restrict__ data,
