@@ -42,9 +42,9 @@
 #define ZP_WIN 128           // LDS header window bytes per frame (multiple of 16)
 #endif
 #define ZP_WIN_CH (ZP_WIN / 16)
-// The window cell index (chunk * 64 + rank) travels in 9 bits of the item
-// descriptor (KEEP_WIN): at most 8 chunks.
-static_assert(ZP_WIN % 16 == 0 && ZP_WIN <= 128, "ZP_WIN must be a multiple of 16, <= 128");
+// The window cell index (chunk * 64 + rank) travels in 10 bits of the item
+// descriptor (KEEP_WIN): at most 16 chunks.
+static_assert(ZP_WIN % 16 == 0 && ZP_WIN <= 256, "ZP_WIN must be a multiple of 16, <= 256");
 #define ZP_GIANT 65536u      // frames longer than this take the exact path
 #ifndef ZP_WAVES
 #define ZP_WAVES 1           // waves per workgroup (independent waves; 1 = finest LDS granularity)
@@ -587,9 +587,10 @@ struct Ranked {          // lane r = frame of rank r
 
 // Per-lane item descriptor.
 #define KEEP_IN (1u << 31)     // chunk belongs to a frame (else past the end)
-#define KEEP_WIN (1u << 30)    // chunk index < 8: window cell in bits 0-8
+#define KEEP_WIN (1u << 30)    // chunk index < ZP_WIN_CH: window cell in bits 0-9
 #define KEEP_TAIL (1u << 29)   // frame's last chunk
-#define KEEP_RANK(k) (((k) >> 10) & 63u)
+#define KEEP_CELL(k) ((k) & 0x3FFu)
+#define KEEP_RANK(k) (((k) >> 16) & 63u)
 
 __device__ __forceinline__ uint32_t bperm(uint32_t v, uint32_t r) {
     return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(r << 2), (int)v);
@@ -666,7 +667,7 @@ __device__ __forceinline__ void issue_group(uint32_t i0, uint32_t nitems, Cursor
         const uint32_t olo = bperm(R.org_lo, r), ohi = bperm(R.org_hi, r);
         const uint32_t lv = bperm(R.last, r), fp = bperm(R.pfx, r);
         const uint32_t ci = vv - fp;                          // chunk index within the frame
-        uint32_t k = (r & 63u) << 10;
+        uint32_t k = (r & 63u) << 16;
         k |= ci < ZP_WIN_CH ? KEEP_WIN | (ci * 64u + ((r ^ ci) & 63u)) : 0u;
         k |= vv == lv ? KEEP_TAIL : 0u;
         keep[q] = (i < nitems && vv <= lv) ? k | KEEP_IN : 0u;
@@ -703,7 +704,7 @@ __device__ __forceinline__ void consume_group(uint32_t i0, uint32_t nitems, int 
         const uint32_t i = i0 + q;
         if (i >= nitems) continue;                            // wave-uniform
         const uint32_t k = keep[q];
-        if (k & KEEP_WIN) win[k & 0x1FFu] = v[q];
+        if (k & KEEP_WIN) win[KEEP_CELL(k)] = v[q];
         uint32_t part = sad16(v[q].x, 0u);
         part = sad16(v[q].y, part);
         part = sad16(v[q].z, part);
