@@ -25,6 +25,7 @@
 #include <stdio.h>
 
 #include "../../include/zero_packet.h"
+#include "zp_stream.h"
 
 extern "C" char* zp__errbuf(void);
 
@@ -43,6 +44,7 @@ extern "C" char* zp__errbuf(void);
 #define ZB_G 16                // lanes per frame: a wave builds 64 / ZB_G frames side by side
 #endif
 #define ZB_F (64 / ZB_G)       // frames per wave
+#define ZB_PENDING 0xFFu       // results[i].err: left by the lane path for the lane-group pass
 
 // Exact reference strings (see zero_packet.h for the cited lines).
 static const char* const kBuildErr[ZP_BERR_COUNT] = {
@@ -163,10 +165,16 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Execution modes of a chain: ZB_M_COOP — a lane group on an LDS copy of
+// the frame; ZB_M_GLOBAL — a lane group in place in global memory (long
+// frames); ZB_M_WIN — one lane on its frame's window in the packed-stream
+// LDS layout (the lane-per-frame path, zp_build_fast_kernel).
+enum { ZB_M_COOP = 0, ZB_M_GLOBAL = 1, ZB_M_WIN = 2 };
+
 // Copies `len` bytes of the data blob to frame offset `at`.
-template <bool COOP, typename P>
+template <int MODE, typename P>
 __device__ void bcopy(BView<P>& v, uint32_t at, const uint8_t* src, uint32_t len, int lane) {
-    if (COOP) {
+    if constexpr (MODE == ZB_M_COOP) {
         for (uint32_t q = lane; q < len; q += ZB_G) v.b[at + q] = src[q];
         wave_sync();
     } else {
@@ -255,12 +263,16 @@ struct OpSrc {
     }
 };
 
+struct NoWin {
+    __device__ uint16_t csum(uint32_t, uint32_t) const { return 0; }
+};
+
 // Executes one chain (all checks of the reference, in its order). Returns
 // the zp_build_err; *hl_out = header_len after the last Ok op, *hw_out = an
 // upper bound of the bytes written ([0, hw)).
-template <bool COOP, typename P>
+template <int MODE, typename P, typename OPS, typename WC>
 __device__ int run_chain(BView<P>& v, const uint8_t ZB_LDSP* stage, uint32_t shift,
-                         const OpSrc& ops, uint32_t nops,
+                         const OPS& ops, uint32_t nops, const WC& wc,
                          const uint8_t* __restrict__ data, int lane, uint32_t* hl_out,
                          uint32_t* done_out, uint32_t* hw_out) {
     int st = BS_RAW;
@@ -368,7 +380,7 @@ __device__ int run_chain(BView<P>& v, const uint8_t ZB_LDSP* stage, uint32_t shi
             if (dl < 6) { e = ZP_BERR_OPTIONS_MIN; break; }             // options.rs:53-68
             if ((uint32_t)s[1] * 8 != dl) { e = ZP_BERR_OPTIONS_MATCH; break; }
             if (2 + dl > sl) { e = ZP_BERR_OPTIONS_EXCEED; break; }
-            bcopy<COOP>(v, hl + 2, d, dl, lane);
+            bcopy<MODE>(v, hl + 2, d, dl, lane);
             hl += ((uint32_t)s[1] + 1) * 8;
             break;
         case ZP_B_ROUTING:                                               // builder.rs:675-704
@@ -379,7 +391,7 @@ __device__ int run_chain(BView<P>& v, const uint8_t ZB_LDSP* stage, uint32_t shi
             if (dl < 4) { e = ZP_BERR_ROUTING_MIN; break; }             // routing.rs:75-94
             if ((uint32_t)s[1] * 8 != dl) { e = ZP_BERR_ROUTING_MATCH; break; }
             if (8 + dl > sl) { e = ZP_BERR_ROUTING_EXCEED; break; }
-            bcopy<COOP>(v, hl + 8, d, dl, lane);
+            bcopy<MODE>(v, hl + 8, d, dl, lane);
             hl += ((uint32_t)s[1] + 1) * 8;
             break;
         case ZP_B_FRAGMENT: {                                            // builder.rs:711-740
@@ -405,12 +417,12 @@ __device__ int run_chain(BView<P>& v, const uint8_t ZB_LDSP* stage, uint32_t shi
             w32(v, hl + 4, o.w[0]);
             w32(v, hl + 8, o.w[1]);
             if (12 + dl > sl) { e = ZP_BERR_AUTH_EXCEED; break; }       // authentication.rs:84-92
-            bcopy<COOP>(v, hl + 12, d, dl, lane);
+            bcopy<MODE>(v, hl + 12, d, dl, lane);
             hl += ((uint32_t)s[1] + 2) * 4;
             break;
         case ZP_B_TCP: case ZP_B_UDP: case ZP_B_ICMPV4: case ZP_B_ICMPV6: {
             const bool v4 = prev == BS_V4 || prev == BS_V4E;            // &[u8; 4] states
-            ext = 20;
+            ext = o.kind == ZP_B_TCP ? 20u : 8u;                        // as chain_extent()
             if (n < hl) {
                 e = o.kind == ZP_B_TCP ? ZP_BERR_TCP_DATA : o.kind == ZP_B_UDP ? ZP_BERR_UDP_DATA
                   : o.kind == ZP_B_ICMPV4 ? ZP_BERR_ICMPV4_DATA : ZP_BERR_ICMPV6_DATA;
@@ -444,18 +456,20 @@ __device__ int run_chain(BView<P>& v, const uint8_t ZB_LDSP* stage, uint32_t shi
                     break;
                 }
                 ext = start + dl > ext ? start + dl : ext;
-                bcopy<COOP>(v, hl + start, d, dl, lane);
+                bcopy<MODE>(v, hl + start, d, dl, lane);
             }
             const uint32_t proto = o.kind == ZP_B_TCP ? 6u : o.kind == ZP_B_UDP ? 17u : 58u;
             const uint32_t acc = o.kind == ZP_B_ICMPV4 ? 0u : pseudo(o, v4, proto, sl);
             const uint32_t at = o.kind == ZP_B_TCP ? 16u : o.kind == ZP_B_UDP ? 6u : 2u;
             w8(v, hl + at, 0); w8(v, hl + at + 1, 0);                    // set_checksum
             uint16_t c;
-            if (COOP) {
+            if constexpr (MODE == ZB_M_COOP) {
                 wave_sync();
                 c = bcsum_lds(stage, shift, hl, n, acc, lane);
-            } else {
+            } else if constexpr (MODE == ZB_M_GLOBAL) {
                 c = bcsum_seq((const uint8_t*)v.b, hl, n, acc);
+            } else {
+                c = wc.csum(hl, acc);
             }
             w16(v, hl + at, c);
             hl += o.kind == ZP_B_TCP ? start : 8u;
@@ -479,7 +493,7 @@ __global__ void ZB_KATTR
 zp_build_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs,
                 const uint32_t* __restrict__ lens, uint64_t n, const zp_build_op* __restrict__ ops,
                 const uint32_t* __restrict__ op_start, const uint8_t* __restrict__ data,
-                zp_build_result* __restrict__ results) {
+                zp_build_result* __restrict__ results, int pending_only) {
     __shared__ __attribute__((aligned(16))) uint8_t lds_all[ZB_WAVES * ZB_F][ZB_LDS];
     __shared__ __attribute__((aligned(16))) zp_build_op lds_ops[ZB_WAVES * ZB_F][ZB_OPS];
     // A group of ZB_G lanes builds one frame; the groups of a wave run side
@@ -488,6 +502,7 @@ zp_build_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs,
     const int slot = threadIdx.x / ZB_G;
     const uint64_t i = (uint64_t)blockIdx.x * ZB_WAVES * ZB_F + slot;
     if (i >= n) return;                              // whole group
+    if (pending_only && results[i].err != ZB_PENDING) return;   // done by the lane path
     const uint32_t len = lens[i];
     uint8_t* const g = arena + offs[i];
     const uint32_t o0 = op_start[i], o1 = op_start[i + 1];
@@ -515,7 +530,8 @@ zp_build_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs,
     if (coop) {
         BView<uint8_t ZB_LDSP*> v{lds + shift, len, true};
         if (o1 >= o0)
-            err = run_chain<true>(v, lds, shift, src, nops, data, lane, &hl, &done, &hw);
+            err = run_chain<ZB_M_COOP>(v, lds, shift, src, nops, NoWin{}, data, lane, &hl, &done,
+                                       &hw);
         if (hw) {
             wave_sync();
             // write back frame bytes [0, hw): whole chunks as 16-B stores, the
@@ -534,7 +550,8 @@ zp_build_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs,
     } else {
         BView<uint8_t*> v{g, len, true};
         if (o1 >= o0)
-            err = run_chain<false>(v, lds, shift, src, nops, data, lane, &hl, &done, &hw);
+            err = run_chain<ZB_M_GLOBAL>(v, lds, shift, src, nops, NoWin{}, data, lane, &hl, &done,
+                                         &hw);
     }
     if (results && lane == 0) {
         zp_build_result r;
@@ -544,6 +561,214 @@ zp_build_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs,
         r.reserved = 0;
         results[i] = r;
     }
+}
+
+
+// ---------------------------------------------------------------------------
+// Lane-per-frame path (zp_build_fast_kernel). A wave takes 64 consecutive
+// frames through the packed stream of the parse kernel (zp_stream.h): every
+// byte read once by full 1 KiB loads, each frame's word sum V of its 16-B
+// chunks, its first ZP_WIN bytes (the window) and last chunk in LDS. Each
+// lane then runs its own chain on its window (ZB_M_WIN) when every byte the
+// chain can touch lies in the window; the L4 checksum comes from the stream
+// sum corrected by the window chunks the chain changed, so the payload is
+// never read a second time. Frames the window cannot hold (long headers,
+// payload copies past it, frames under 64 B or over 64 KiB) are marked
+// ZB_PENDING and built by the lane-group kernel in a second launch.
+// ---------------------------------------------------------------------------
+
+// A lane's chain in global memory (address space 1: the compiler knows these
+// loads cannot alias the LDS stores of the chain and may issue them early).
+struct OpGlobal {
+    const zp_build_op* g;
+    __device__ __forceinline__ zp_build_op get(uint32_t k) const {
+        const ZP_GLOBAL zp_u32x4* q = (const ZP_GLOBAL zp_u32x4*)(g + k);
+        const zp_u32x4 t[4] = {q[0], q[1], q[2], q[3]};
+        zp_build_op o;
+        __builtin_memcpy(&o, t, sizeof o);
+        return o;
+    }
+    __device__ __forceinline__ uint32_t kind(uint32_t k) const {
+        return *(const ZP_GLOBAL uint8_t*)(g + k);
+    }
+};
+
+__device__ __forceinline__ uint32_t sad4(uint4 q) {
+    return sad16(q.w, sad16(q.z, sad16(q.y, sad16(q.x, 0u))));
+}
+
+// After the stream each lane copies its window out of the swizzled
+// [chunk][rank] cells into a private contiguous region of the same LDS
+// (ZB_RSTRIDE = 33 dwords per lane: the lanes' accesses to a same offset
+// fall in 64 different banks), so the chain addresses bytes directly.
+#define ZB_RSTRIDE 132
+static_assert(64 * ZB_RSTRIDE <= (ZP_WIN_CH + 1) * 64 * 16, "regions must fit the window LDS");
+
+__device__ __forceinline__ uint4 ld_region(const uint8_t ZB_LDSP* r, uint32_t at) {
+    const uint32_t ZB_LDSP* d = (const uint32_t ZB_LDSP*)(r + at);
+    return make_uint4(d[0], d[1], d[2], d[3]);
+}
+
+// internet_checksum(bytes[l4 .. len], acc) (checksum.rs:5-29) from the
+// stream: V of the frame's chunks with the window chunks' changes applied,
+// minus the chunks before l4 and the bytes past the frame end. With V the
+// word sum at even ARENA addresses, the reference's word sum W satisfies
+// W = V (segment starts at an odd address) or W == 256 V (mod 65535); the
+// fold of S = acc + W depends only on S mod 65535 and on S == 0 (exact for
+// frames up to 64 KiB, the only ones this path takes).
+struct WinCsum {
+    const uint8_t ZB_LDSP* region;    // the lane's window, from A & ~15
+    uint4 tail;                       // the frame's last chunk (original bytes)
+    uintptr_t ga;
+    uint32_t shift, len, nchw, fsum;
+    uint32_t vorig[ZP_WIN_CH];
+    __device__ uint16_t csum(uint32_t l4, uint32_t acc) const {
+        const uint32_t y4 = l4 + shift, c4 = y4 >> 4;
+        uint32_t vall = fsum, before = 0;
+#pragma unroll
+        for (uint32_t c = 0; c < ZP_WIN_CH; ++c) {
+            if (c < nchw) {
+                const uint4 q = ld_region(region, 16 * c);
+                const uint32_t vn = sad4(q);
+                vall += vn - vorig[c];
+                if (c < c4) before += vn;
+                else if (c == c4) before += range_sum(q, 0, y4 & 15);
+            }
+        }
+        const uint32_t he = (len + shift) & 15u;
+        const uint32_t ex = he ? range_sum(tail, he, 16u) : 0u;
+        const uint32_t V = vall - before - ex;
+        if (acc == 0 && V == 0) return 0xFFFF;             // S == 0: !fold(0)
+        uint32_t w = V % 65535u;
+        if (!((ga + l4) & 1)) w = (w * 256u) % 65535u;
+        const uint32_t r = (acc % 65535u + w) % 65535u;
+        return (uint16_t)~(r ? r : 65535u);
+    }
+};
+
+// Upper bound of the bytes a chain can read or write (from its ops alone;
+// the offsets the writers derive from the buffer are the values the chain
+// itself wrote: ihl, data offset, extension lengths).
+__device__ uint32_t chain_extent(const OpGlobal& ops, uint32_t nops) {
+    uint32_t hl = 0, top = 0;
+    for (uint32_t k = 0; k < nops; ++k) {
+        const zp_build_op o = ops.get(k);
+        const uint32_t dl = o.data_len != ZP_BUILD_NO_DATA ? o.data_len : 0u;
+        uint32_t ext = 0, adv = 0;
+        switch (o.kind) {
+        case ZP_B_ETHERNET: case ZP_B_ETHERNET_VLAN: case ZP_B_ETHERNET_QINQ:
+            ext = 22; hl = 0;
+            adv = o.kind == ZP_B_ETHERNET ? 14 : o.kind == ZP_B_ETHERNET_VLAN ? 18 : 22;
+            break;
+        case ZP_B_ARP: ext = 28; adv = 28; break;
+        case ZP_B_IPV4: adv = (o.b[1] & 15u) * 4; ext = adv > 20 ? adv : 20; break;
+        case ZP_B_IPV6: ext = 40; adv = 40; break;
+        case ZP_B_HOP_BY_HOP: case ZP_B_DEST_OPTS1: case ZP_B_DEST_OPTS2:
+            ext = 2 + dl; adv = ((uint32_t)o.b[1] + 1) * 8; break;
+        case ZP_B_ROUTING: ext = 8 + dl; adv = ((uint32_t)o.b[1] + 1) * 8; break;
+        case ZP_B_FRAGMENT: ext = 8; adv = 8; break;
+        case ZP_B_AUTH: ext = 12 + dl; adv = ((uint32_t)o.b[1] + 2) * 4; break;
+        case ZP_B_TCP: {
+            const uint32_t st = (o.b[0] & 15u) * 4;
+            ext = st + dl > 20 ? st + dl : 20; adv = st; break;
+        }
+        default: ext = 8 + dl; adv = 8; break;           // UDP, ICMPv4, ICMPv6
+        }
+        top = hl + ext > top ? hl + ext : top;
+        hl += adv;
+        if (hl > 0x100000u) return ~0u;                  // no window holds that
+    }
+    return top;
+}
+
+#ifndef ZB_FAST_WPE
+#define ZB_FAST_WPE 1
+#endif
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZB_FAST_WPE)))
+zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs,
+                     const uint32_t* __restrict__ lens, uint64_t n,
+                     const zp_build_op* __restrict__ ops, const uint32_t* __restrict__ op_start,
+                     const uint8_t* __restrict__ data, zp_build_result* __restrict__ results) {
+    __shared__ WaveLds lds;
+    const int lane = threadIdx.x & 63;
+    const uint64_t t = blockIdx.x;
+    if (t * 64 >= n) return;
+    const uintptr_t fallback = (uintptr_t)&zp_safe_chunk;
+    uint4* win = &lds.win[0];
+    uint4* tail = &lds.win[ZP_WIN_CH * 64];
+    uint32_t len;
+    uintptr_t ga;
+    load_desc(arena, offs, lens, n, t, lane, len, ga);
+    TileState s;
+    tile_setup(s, t, len, ga, n, lane, lds);
+    uint4 va[ZP_G];
+    uint32_t ka[ZP_G];
+    issue_group<ZP_G>(0, s.nitems, s.cur, s.R, lane, fallback, va, ka);
+    consume_group<ZP_G>(0, s.nitems, lane, va, ka, win, tail, lds.cend, s.run);
+    for (uint32_t i0 = ZP_G; i0 < s.nitems; i0 += ZP_G) {
+        issue_group<ZP_G>(i0, s.nitems, s.cur, s.R, lane, fallback, va, ka);
+        consume_group<ZP_G>(i0, s.nitems, lane, va, ka, win, tail, lds.cend, s.run);
+    }
+    wave_lds_fence();                                  // windows written by other lanes
+    if (!s.live) return;
+    const uint64_t i = t * 64 + lane;
+    const uint32_t o0 = op_start[i], o1 = op_start[i + 1];
+    const uint32_t nops = o1 >= o0 ? o1 - o0 : 0u;
+    const OpGlobal og{ops + o0};
+    const bool fast = o1 >= o0 && len >= 64 && !s.giant && chain_extent(og, nops) <= s.wlen;
+    if (!fast) {
+        zp_build_result r;
+        r.header_len = 0; r.err = (uint8_t)ZB_PENDING; r.ops_done = 0; r.reserved = 0;
+        results[i] = r;
+        return;
+    }
+    const uint32_t rank = s.rank & 63u;
+    const uint32_t nch = (len + s.shift + 15) >> 4;
+    WinCsum wc;
+    wc.ga = s.ga;
+    wc.shift = s.shift;
+    wc.len = len;
+    wc.nchw = nch < ZP_WIN_CH ? nch : ZP_WIN_CH;
+    wc.fsum = lds.cend[s.rank] - (s.rank ? lds.cend[s.rank - 1] : 0u);
+    wc.tail = tail[rank];
+    uint4 cells[ZP_WIN_CH];
+#pragma unroll
+    for (uint32_t c = 0; c < ZP_WIN_CH; ++c) {
+        cells[c] = c < wc.nchw ? win[c * 64 + ((rank ^ c) & 63u)] : make_uint4(0, 0, 0, 0);
+        wc.vorig[c] = sad4(cells[c]);
+    }
+    wave_lds_fence();                                  // every lane holds its cells
+    uint8_t ZB_LDSP* region = (uint8_t ZB_LDSP*)win + lane * ZB_RSTRIDE;
+#pragma unroll
+    for (uint32_t c = 0; c < ZP_WIN_CH; ++c) {
+        uint32_t ZB_LDSP* d = (uint32_t ZB_LDSP*)(region + 16 * c);
+        d[0] = cells[c].x; d[1] = cells[c].y; d[2] = cells[c].z; d[3] = cells[c].w;
+    }
+    wc.region = region;
+    BView<uint8_t ZB_LDSP*> v{region + s.shift, len, true};
+    uint32_t hl = 0, done = 0, hw = 0;
+    const int err = run_chain<ZB_M_WIN>(v, (const uint8_t ZB_LDSP*)nullptr, s.shift, og, nops, wc,
+                                        data, lane, &hl, &done, &hw);
+    // write back frame bytes [0, hw) from the region: whole 16-B chunks as
+    // one store, edge chunks byte by byte (never a neighbour's byte)
+    const uintptr_t a0 = s.ga & ~(uintptr_t)15;
+    const uint32_t end = s.shift + (hw < s.wlen ? hw : s.wlen);   // hw <= extent <= wlen
+    for (uint32_t c = 0; c < ((end + 15) >> 4); ++c) {
+        const uint32_t lo = 16 * c, hi = lo + 16;
+        if (lo >= s.shift && hi <= end) {
+            const uint4 q = ld_region(region, lo);
+            *(ZP_GLOBAL zp_u32x4*)(a0 + lo) = zp_u32x4{q.x, q.y, q.z, q.w};
+        } else {
+            for (uint32_t b = lo < s.shift ? s.shift : lo; b < (hi < end ? hi : end); ++b)
+                *(ZP_GLOBAL uint8_t*)(a0 + b) = region[b];
+        }
+    }
+    zp_build_result r;
+    r.header_len = hl;
+    r.err = (uint8_t)err;
+    r.ops_done = (uint8_t)(done > 255 ? 255 : done);
+    r.reserved = 0;
+    results[i] = r;
 }
 
 extern "C" int zp_build_batch_device(uint8_t* arena, const uint64_t* offs, const uint32_t* lens,
@@ -557,12 +782,26 @@ extern "C" int zp_build_batch_device(uint8_t* arena, const uint64_t* offs, const
     }
     const uint64_t per_block = (uint64_t)ZB_WAVES * ZB_F;
     const uint64_t blocks = (n + per_block - 1) / per_block;
-    if (blocks > 0x7FFFFFFFull) {
+    const uint64_t fast_blocks = (n + 63) / 64;
+    if (blocks > 0x7FFFFFFFull || fast_blocks > 0x7FFFFFFFull) {
         snprintf(zp__errbuf(), 256, "zp_build_batch_device: batch too large");
         return -1;
     }
-    hipLaunchKernelGGL(zp_build_kernel, dim3((unsigned)blocks), dim3(64 * ZB_WAVES), 0,
-                       (hipStream_t)stream, arena, offs, lens, n, ops, op_start, data, results);
+    hipStream_t st = (hipStream_t)stream;
+    // The lane-per-frame pass needs a per-frame "pending" mark: the results
+    // array, or a stream-ordered scratch copy when the caller passes none.
+    zp_build_result* res = results;
+    if (!res && hipMallocAsync((void**)&res, n * sizeof(zp_build_result), st) != hipSuccess) {
+        snprintf(zp__errbuf(), 256, "zp_build_batch_device: scratch allocation failed");
+        return -2;
+    }
+    hipLaunchKernelGGL(zp_build_fast_kernel, dim3((unsigned)fast_blocks), dim3(64), 0, st, arena,
+                       offs, lens, n, ops, op_start, data, res);
+#ifndef ZB_ABL_NO_SECOND   // timing ablation only (tools/build_variants.sh)
+    hipLaunchKernelGGL(zp_build_kernel, dim3((unsigned)blocks), dim3(64 * ZB_WAVES), 0, st, arena,
+                       offs, lens, n, ops, op_start, data, res, 1);
+#endif
+    if (!results) (void)hipFreeAsync(res, st);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         snprintf(zp__errbuf(), 256, "zp_build_kernel launch: %s", hipGetErrorString(e));

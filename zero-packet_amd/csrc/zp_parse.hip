@@ -526,18 +526,6 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
     }
 }
 
-// Descriptor loads are unconditional (clamped index, masked after): a load
-// count that depends on the lane's branch turns later waits into vmcnt(0).
-__device__ __forceinline__ void load_desc(const uint8_t* arena, const uint64_t* offs,
-                                          const uint32_t* lens, uint64_t n, uint64_t tile,
-                                          int lane, uint32_t& len, uintptr_t& ga) {
-    const uint64_t p = tile * 64 + lane;
-    const uint64_t pc = p < n ? p : n - 1;
-    const uint32_t l = lens[pc];
-    const uint64_t o = offs[pc];
-    len = p < n ? l : 0u;
-    ga = (uintptr_t)arena + (p < n ? o : 0);
-}
 
 // One wave per tile; the hardware back-fills finished waves with the next
 // tiles in dispatch order, so the resident waves always stream a contiguous

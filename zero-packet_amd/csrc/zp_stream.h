@@ -344,3 +344,16 @@ __device__ __forceinline__ void wave_lds_fence() {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+
+// Descriptor loads are unconditional (clamped index, masked after): a load
+// count that depends on the lane's branch turns later waits into vmcnt(0).
+__device__ __forceinline__ void load_desc(const uint8_t* arena, const uint64_t* offs,
+                                          const uint32_t* lens, uint64_t n, uint64_t tile,
+                                          int lane, uint32_t& len, uintptr_t& ga) {
+    const uint64_t p = tile * 64 + lane;
+    const uint64_t pc = p < n ? p : n - 1;
+    const uint32_t l = lens[pc];
+    const uint64_t o = offs[pc];
+    len = p < n ? l : 0u;
+    ga = (uintptr_t)arena + (p < n ? o : 0);
+}
