@@ -372,3 +372,53 @@ def test_gpu_builder_reference_vectors(zp, golden):
     a = arena.cpu().numpy()
     for (name, l_, _), o, r in zip(cases, offs, res):
         assert r["err"] == 0 and a[o:o + l_].tobytes() == vec[name], name
+
+
+@pytest.mark.gpu
+def test_gpu_builder_lane_path_edges(zp):
+    """The lane-per-frame path at its edges: every frame alignment (0-15),
+    payload copies ending exactly at / one byte past the 128-B window, frames
+    of exactly 64 B, all-zero ICMPv4 segments (S == 0 -> checksum 0xFFFF) and
+    segments whose sum folds to 0xFFFF; byte-exact vs the oracle."""
+    import torch
+    C = zp.builder.Chain
+    chains, lens, fills = [], [], []
+    for shift in range(16):
+        wlen = 128 - shift
+        for extra in (-1, 0, 1):
+            pay = bytes(range(1, wlen - 42 + extra + 1)) if wlen - 42 + extra > 0 else b""
+            chains.append(C().ethernet(M1, M2, 2048).ipv4(4, 5, 0, 0, 186, 7, 0, 0, 64, 17, IP1, IP2)
+                          .udp(IP1, 5, IP2, 6, 166, pay))
+            lens.append(200)
+            fills.append(np.full(200, 0xAB, np.uint8))
+        chains.append(C().ethernet([0] * 6, [0] * 6, 2048).ipv4(4, 5, 0, 0, 50, 0, 0, 0, 0, 1,
+                                                                [0] * 4, [0] * 4).icmpv4(0, 0))
+        lens.append(64)
+        fills.append(np.zeros(64, np.uint8))
+        chains.append(C().ethernet(M1, M2, 34525).ipv6(6, 0, 0, 0, 58, 1, S6, D6)
+                      .icmpv6(S6, D6, 128, 0, b"\xff\xff" * 3))
+        lens.append(64 + shift)
+        fills.append(np.full(64 + shift, 0xFF, np.uint8))
+    # every frame starts at a different offset mod 16
+    offs, pos = [], 0
+    for k, l_ in enumerate(lens):
+        pos += (k % 16 - pos % 16) % 16
+        offs.append(pos)
+        pos += l_
+    batch = zp.builder.BuildBatch()
+    for c in chains:
+        batch.add(c)
+    ops, op_start, data = batch.pack()
+    arena = np.zeros(pos + 64, np.uint8)
+    for o, l_, f in zip(offs, lens, fills):
+        arena[o:o + l_] = f
+    want = arena.copy()
+    wres = orc.build_batch(want, np.array(offs, np.uint64), np.array(lens, np.uint32), ops,
+                           op_start, data).view(zp.builder.RESULT_DTYPE).reshape(-1)
+    d = torch.device("cuda:0")
+    ta = torch.from_numpy(arena).to(d)
+    got = batch.run(ta, torch.tensor(offs, dtype=torch.int64, device=d),
+                    torch.tensor(lens, dtype=torch.int32, device=d))
+    torch.cuda.synchronize()
+    assert ta.cpu().numpy().tobytes() == want.tobytes()
+    assert got.tobytes() == wres.tobytes()
