@@ -41,7 +41,28 @@ struct zp_ctx {
     uint32_t* h_lens[SLOTS];
     zp_record* h_rec[SLOTS];
     zp_ext_offsets* h_ext[SLOTS];
+    // zp_build_batch_host scratch, allocated on first use and grown as needed
+    zp_build_op* d_bops;
+    uint64_t bops_cap;
+    uint8_t* d_bdata;
+    uint64_t bdata_cap;
+    uint32_t* d_bstart;
+    zp_build_result* d_bres;
+    uint32_t* h_bstart;
 };
+
+// Grows a device buffer to at least `need` elements (contents not kept).
+template <typename T>
+static hipError_t grow(T** p, uint64_t* cap, uint64_t need) {
+    if (*p && *cap >= need) return hipSuccess;
+    (void)hipFree(*p);
+    *p = NULL;
+    *cap = 0;
+    const uint64_t n = need < 64 ? 64 : need + need / 4;
+    const hipError_t e = hipMalloc((void**)p, n * sizeof(T));
+    if (e == hipSuccess) *cap = n;
+    return e;
+}
 
 #define TRY(x)                                                                     \
     do {                                                                           \
@@ -68,6 +89,8 @@ extern "C" void zp_ctx_destroy(zp_ctx* c) {
         if (c->ev[k]) (void)hipEventDestroy(c->ev[k]);
         if (c->s[k]) (void)hipStreamDestroy(c->s[k]);
     }
+    (void)hipFree(c->d_bops); (void)hipFree(c->d_bdata); (void)hipFree(c->d_bstart);
+    (void)hipFree(c->d_bres); (void)hipHostFree(c->h_bstart);
     (void)hipSetDevice(prev);
     free(c);
 }
@@ -330,19 +353,20 @@ extern "C" int zp_build_batch_host(zp_ctx* c, uint8_t* arena, uint64_t arena_byt
     (void)hipGetDevice(&prev);
     if (hipSetDevice(c->device) != hipSuccess) return -2;
     int rc = 0;
-    zp_build_op* d_ops = NULL;
-    uint32_t* d_start = NULL;
-    uint8_t* d_data = NULL;
-    zp_build_result* d_res = NULL;
-    uint32_t* h_start = NULL;
     const uint64_t nops = op_start[n] - op_start[0];
     hipStream_t s = c->s[0];
-    hipError_t e = hipMalloc(&d_ops, (nops ? nops : 1) * sizeof(zp_build_op));
-    if (e == hipSuccess) e = hipMalloc(&d_start, (c->chunk_pkts + 1) * sizeof(uint32_t));
-    if (e == hipSuccess) e = hipMalloc(&d_data, data_bytes ? data_bytes : 16);
-    if (e == hipSuccess) e = hipMalloc(&d_res, c->chunk_pkts * sizeof(zp_build_result));
-    if (e == hipSuccess) e = hipHostMalloc(&h_start, (c->chunk_pkts + 1) * sizeof(uint32_t),
-                                           hipHostMallocDefault);
+    hipError_t e = grow(&c->d_bops, &c->bops_cap, nops ? nops : 1);
+    if (e == hipSuccess) e = grow(&c->d_bdata, &c->bdata_cap, data_bytes ? data_bytes : 16);
+    if (e == hipSuccess && !c->d_bstart) e = hipMalloc(&c->d_bstart, (c->chunk_pkts + 1) * 4);
+    if (e == hipSuccess && !c->d_bres)
+        e = hipMalloc(&c->d_bres, c->chunk_pkts * sizeof(zp_build_result));
+    if (e == hipSuccess && !c->h_bstart)
+        e = hipHostMalloc(&c->h_bstart, (c->chunk_pkts + 1) * 4, hipHostMallocDefault);
+    zp_build_op* d_ops = c->d_bops;
+    uint32_t* d_start = c->d_bstart;
+    uint8_t* d_data = c->d_bdata;
+    zp_build_result* d_res = c->d_bres;
+    uint32_t* h_start = c->h_bstart;
     if (e == hipSuccess && nops)
         e = hipMemcpyAsync(d_ops, ops + op_start[0], nops * sizeof(zp_build_op),
                            hipMemcpyHostToDevice, s);
@@ -400,8 +424,6 @@ extern "C" int zp_build_batch_host(zp_ctx* c, uint8_t* arena, uint64_t arena_byt
     if (rc == -2 && e != hipSuccess)
         snprintf(g_ctx_error, ERRBUF_LEN, "zp_build_batch_host: %s", hipGetErrorString(e));
     (void)hipStreamSynchronize(s);
-    (void)hipFree(d_ops); (void)hipFree(d_start); (void)hipFree(d_data); (void)hipFree(d_res);
-    (void)hipHostFree(h_start);
     (void)hipSetDevice(prev);
     return rc;
 }
