@@ -270,30 +270,37 @@ def test_host_path_multi(zp, golden):
     assert_same(rec, ext, want, wext)
 
 
-# ---- full-size C3 properties ----------------------------------------------
+# ---- full-size properties (BASELINE configs 3-5) ----------------------------
 
-def test_full_size_c3_properties(zp):
-    """BASELINE config 3 at full size (16M frames, ~13 GB): every frame
-    accepted, a 200k random sample byte-exact vs the oracle, idempotent
-    re-parse, and flipping one L4 byte per frame turns every record into the
-    checksum error."""
-    n = 16 * 1024 * 1024
-    arena, offs, lens = zp.batch.generate("c3", n, device=dev())
+@pytest.mark.parametrize("config,n", [("c3", 16 << 20), ("c4", 16 << 20), ("c5", 32 << 20)])
+def test_full_size_properties(zp, config, n):
+    """BASELINE configs 3-5 at full per-GPU size (c3/c4: 16M frames; c5: one
+    GPU's shard of the 256M IMIX = 32M frames): every frame accepted, a
+    random sample byte-exact vs the oracle, idempotent re-parse, and flipping
+    one bit of every frame's last byte turns every record into the L4
+    checksum error of its innermost IP version."""
+    from importlib import import_module
+    rec = import_module("zero-packet_amd.records")
+    arena, offs, lens = zp.batch.generate(config, n, device=dev())
     r1, e1 = zp.batch.parse_batch(arena, offs, lens)
-    err = r1[:, 4]
-    assert int((err != 0).sum()) == 0
-    r2, _ = zp.batch.parse_batch(arena, offs, lens)
-    assert torch.equal(r1, r2)
+    assert int((r1[:, 4] != 0).sum()) == 0
+    r2, e2 = zp.batch.parse_batch(arena, offs, lens)
+    assert torch.equal(r1, r2) and torch.equal(e1, e2)
     idx = torch.randint(0, n, (2000,), device=arena.device, generator=torch.Generator(
         device=arena.device).manual_seed(1))
     so, sl = offs[idx].cpu().numpy(), lens[idx].cpu().numpy()
-    frames = [arena[int(o):int(o) + int(l)].cpu().numpy() for o, l in zip(so[:2000], sl[:2000])]
+    frames = [arena[int(o):int(o) + int(l)].cpu().numpy() for o, l in zip(so, sl)]
     sa, sof, sle = pack([f.tobytes() for f in frames])
     want, wext = orc.parse_batch(sa, sof, sle)
-    got, gext = zp.batch.records_to_numpy(r1[idx[:2000]], e1[idx[:2000]])
+    got, gext = zp.batch.records_to_numpy(r1[idx], e1[idx])
     assert_same(got, gext, want, wext)
+    flags = r1[:, 0:4].contiguous().view(torch.int32)[:, 0]
+    ipip = (flags & rec.F_IP_IN_IP) != 0
+    v6 = torch.where(ipip, (flags & rec.F_IP_IN_IP_V6) != 0, (flags & rec.F_IPV6) != 0)
+    want_err = torch.where(v6, ERR["IPV6_L4_CHECKSUM"], ERR["IPV4_L4_CHECKSUM"]).to(torch.uint8)
+    del r2, e2
     last = offs + lens.to(torch.int64) - 1
     arena[last] ^= 1
     r3, _ = zp.batch.parse_batch(arena, offs, lens)
     torch.cuda.synchronize()
-    assert bool((r3[:, 4] == ERR["IPV4_L4_CHECKSUM"]).all())
+    assert torch.equal(r3[:, 4], want_err)

@@ -269,7 +269,15 @@ __device__ __forceinline__ void consume_group(uint32_t i0, uint32_t nitems, int 
         part = sad16(v[q].y, part);
         part = sad16(v[q].z, part);
         part = sad16(v[q].w, part);
+#ifdef ZP_ABL_NOSCAN
+        const uint32_t P = k & KEEP_IN ? part : 0u;           // timing ablation only
+#else
         const uint32_t P = wave_scan(k & KEEP_IN ? part : 0u);
+#endif
+#ifdef ZP_ABL_EXTRA
+#pragma unroll
+        for (int x = 0; x < ZP_ABL_EXTRA; ++x) asm volatile("v_add_u32 %0, %0, 1" : "+v"(part));
+#endif
         if (k & KEEP_TAIL) {
             tail[KEEP_RANK(k)] = v[q];
             cend[KEEP_RANK(k)] = run + P;
