@@ -240,6 +240,15 @@ __device__ uint32_t sumW_exact(FrameView& f, uint32_t lo, uint32_t hi) {
 #endif
 }
 
+// Pseudo-header word sum modulo 65535. For frames of <= 64 KiB the verdict
+// (csum_ok) sees the accumulator only as acc mod 65535, and acc >= proto +
+// length > 0 (no zero test involved); only jumbo frames, which reproduce the
+// reference's u32 wrap-around, need sumW_exact.
+__device__ __forceinline__ uint32_t sumW_mod(FrameView& f, uint32_t lo, uint32_t hi) {
+    const uint32_t V = sumV(f, lo, hi);
+    return (((uintptr_t)f.g + lo) & 1) ? V : V * 256u;   // == W (mod 65535)
+}
+
 // Exact reference checksum for long segments: sums even/odd-address bytes
 // separately and reproduces the u32 wrap of checksum.rs:12 (release build).
 __device__ bool csum_ok_exact(const uint8_t* g, uint32_t lo, uint32_t hi, uint32_t acc) {
@@ -364,7 +373,11 @@ __device__ void walk_frame(FrameView& f, Walk& w) {
                     if (ihl < 20) { err = ZP_ERR_IPV4_IHL_TOO_SHORT; goto done; }
                     if (sl < ihl) { err = ZP_ERR_IPV4_HDR_TOO_LONG; goto done; }
                     if (rd16(f, pos + 2) != sl) { err = ZP_ERR_IPV4_TOTAL_LENGTH; goto done; }
+#ifdef ZP_ABL_NO_IPSUM
+                    const uint32_t hv = 65535u;                        // timing ablation only
+#else
                     const uint32_t hv = sumV(f, pos, pos + ihl);       // ipv4.rs:262-264
+#endif
                     if (!(hv != 0 && hv % 65535u == 0)) { err = ZP_ERR_IPV4_CHECKSUM; goto done; }
                     proto = rd8(f, pos + 9);
                     pp = pos + ihl;
@@ -430,8 +443,17 @@ __device__ void walk_frame(FrameView& f, Walk& w) {
                 // Pseudo-header of the innermost IP only (outer levels of an
                 // IP-in-IP chain never need one): parser.rs:316-333 (IPv4;
                 // none for ICMPv4), parser.rs:341-361 (IPv6, final next header).
-                w.acc = v4 ? (proto == 1 ? 0u : sumW_exact(f, pos + 12, pos + 20) + proto + (len - pp))
-                           : sumW_exact(f, pos + 8, pos + 40) + proto + (len - pp);
+// One pseudo-header sum for both IP versions (the address range differs,
+                // the code does not: no divergent duplicate).
+#ifdef ZP_ABL_NO_PSEUDO
+                const uint32_t ps = 0;                                // timing ablation only
+#else
+                const uint32_t plo = v4 ? pos + 12 : pos + 8, phi = v4 ? pos + 20 : pos + 40;
+                uint32_t ps;
+                if (len > ZP_GIANT) ps = sumW_exact(f, plo, phi);
+                else ps = sumW_mod(f, plo, phi);
+#endif
+                w.acc = (v4 && proto == 1) ? 0u : ps + proto + (len - pp);
                 r.l4_off = pp;
                 w.pending = 1;
                 w.l4 = pp;
@@ -506,7 +528,11 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
             const uint32_t fsum = lds.cend[r] - (r ? lds.cend[r - 1] : 0u);
             const uint32_t he = (s.len + s.shift) & 15u;    // bytes of the last chunk in use
             const uint32_t ex = he ? range_sum(tail[r], he, 16u) : 0u;
+#ifdef ZP_ABL_NO_L4HDR
+            ok = csum_ok(w.acc, fsum - ex, odd);                  // timing ablation only
+#else
             ok = csum_ok(w.acc, fsum - sumV(fv, 0, w.l4) - sum_head(fv) - ex, odd);
+#endif
         }
         if (!ok) {
             rec = zp_record{};
