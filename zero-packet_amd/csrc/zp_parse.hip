@@ -196,16 +196,41 @@ __device__ void sum_vb(FrameView& f, uint32_t lo, uint32_t hi, uint32_t& V, uint
     }
 }
 
-// Arena-parity word sum V of frame bytes [lo, hi).
+// Chunk c (from A & ~15) of the frame: the LDS window, then global.
+__device__ __forceinline__ uint4 chunk_at(FrameView& f, uint32_t c) {
+    return c < ZP_WIN_CH ? win_chunk(f, c) : fb_chunk(f, c);
+}
+
+// V-sum of bytes [0, k) of a 16-B chunk (0 <= k <= 16): running v_sad_u16
+// over the whole dwords, one bitfield extract for the partial one.
+__device__ __forceinline__ uint32_t chunk_prefix(uint4 v, uint32_t k) {
+    const uint32_t s1 = sad16(v.x, 0u), s2 = sad16(v.y, s1), s3 = sad16(v.z, s2);
+    const uint32_t d = k >> 2;
+    const uint32_t full = d == 0 ? 0u : d == 1 ? s1 : d == 2 ? s2 : d == 3 ? s3 : sad16(v.w, s3);
+    const uint32_t x = d == 0 ? v.x : d == 1 ? v.y : d == 2 ? v.z : v.w;
+    return sad16(__builtin_amdgcn_ubfe(x, 0u, (k & 3u) * 8u), full);
+}
+
+// Arena-parity word sum V of frame bytes [lo, hi) (hi <= len): whole chunks
+// [c0, c1) plus the prefix of chunk c1 minus the prefix of chunk c0 (no
+// per-byte masks; every chunk read holds a byte of the range).
 __device__ __forceinline__ uint32_t sumV(FrameView& f, uint32_t lo, uint32_t hi) {
-    uint32_t V, B;
-    sum_vb<false>(f, lo, hi, V, B);
+    if (lo >= hi) return 0u;
+    const uint32_t ylo = lo + f.shift, yhi = hi + f.shift;
+    const uint32_t c0 = ylo >> 4, c1 = (yhi - 1) >> 4;
+    uint32_t V = chunk_prefix(chunk_at(f, c1), yhi - 16u * c1) -
+                 chunk_prefix(chunk_at(f, c0), ylo & 15u);
+    for (uint32_t c = c0; c < c1; ++c) V = chunk_sum(chunk_at(f, c), 0, 16, V);
     return V;
 }
 
-// V-sum of the bytes [A & ~15, A) that precede the frame in its first chunk.
-__device__ __forceinline__ uint32_t sum_head(const FrameView& f) {
-    return f.shift ? chunk_sum(win_chunk(f, 0), 0, (int)f.shift, 0u) : 0u;
+// V-sum of the bytes [A & ~15, A + x) (the frame's first x bytes and the
+// bytes before it in its first chunk).
+__device__ __forceinline__ uint32_t sum_to(FrameView& f, uint32_t x) {
+    const uint32_t y = x + f.shift, cx = y >> 4;
+    uint32_t V = (y & 15u) ? chunk_prefix(chunk_at(f, cx), y & 15u) : 0u;
+    for (uint32_t c = 0; c < cx; ++c) V = chunk_sum(chunk_at(f, c), 0, 16, V);
+    return V;
 }
 
 // Exact big-endian word sum (reference parity: words start at lo) of frame
@@ -531,7 +556,7 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
 #ifdef ZP_ABL_NO_L4HDR
             ok = csum_ok(w.acc, fsum - ex, odd);                  // timing ablation only
 #else
-            ok = csum_ok(w.acc, fsum - sumV(fv, 0, w.l4) - sum_head(fv) - ex, odd);
+            ok = csum_ok(w.acc, fsum - sum_to(fv, w.l4) - ex, odd);
 #endif
         }
         if (!ok) {
