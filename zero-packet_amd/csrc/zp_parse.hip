@@ -37,6 +37,16 @@
 #include "../../include/zero_packet.h"
 #include "../../include/zero_packet_errstr.h"
 #include "zp_cols.h"
+// Parse-kernel geometry: a 112-B header window (7 KiB of LDS per wave) and
+// at most 96 VGPRs, so 18 waves fit a CU instead of 16. Measured per
+// placement in one process against the 128-B window at 108 VGPRs: c5 -6 %,
+// c3 and c4 within +-1 %.
+#ifndef ZP_WIN
+#define ZP_WIN 112
+#endif
+#ifndef ZP_WPE
+#define ZP_WPE 5
+#endif
 #include "zp_stream.h"
 
 #ifndef ZP_WAVES
@@ -587,6 +597,9 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
 #else
 #define ZP_KATTR __launch_bounds__(64 * ZP_WAVES)
 #endif
+// The fused parse + columns kernel carries the column getters too: no
+// waves-per-EU bound (at 96 VGPRs it spills).
+#define ZP_KATTR_COLS __launch_bounds__(64 * ZP_WAVES)
 template <bool COLS>
 __device__ __forceinline__ void parse_tiles(const uint8_t* __restrict__ arena,
                                             const uint64_t* __restrict__ offs,
@@ -651,7 +664,7 @@ zp_parse_kernel(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ 
 }
 
 // Parse + column views in one pass (zp_parse_batch_columns_device).
-__global__ void ZP_KATTR
+__global__ void ZP_KATTR_COLS
 zp_parse_columns_kernel(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs,
                         const uint32_t* __restrict__ lens, uint64_t n,
                         zp_record* __restrict__ records, zp_ext_offsets* __restrict__ inner_ext,
