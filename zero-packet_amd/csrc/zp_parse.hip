@@ -134,8 +134,20 @@ __device__ __forceinline__ uint32_t win_dw(const FrameView& f, uint32_t d) {
 // Chunk c (from A & ~15) past the window: one 16-B load per distinct chunk
 // (deep IPv6 extension chains and IP-in-IP read a few bytes each from the
 // same chunks).
+#ifdef ZP_DBG_FBCOUNT   // diagnostic build only (tools/fbcount.py): fallback chunk loads
+__device__ unsigned long long zp_fb_count;
+extern "C" unsigned long long zp_dbg_fb_count(void) {
+    unsigned long long v = 0, z = 0;
+    (void)hipMemcpyFromSymbol(&v, HIP_SYMBOL(zp_fb_count), sizeof v);
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(zp_fb_count), &z, sizeof z);
+    return v;
+}
+#endif
 __device__ __forceinline__ uint4 fb_chunk(FrameView& f, uint32_t c) {
     if (c != f.xi) {
+#ifdef ZP_DBG_FBCOUNT
+        atomicAdd(&zp_fb_count, 1ull);
+#endif
         f.xc = ldg16(((uintptr_t)f.g & ~(uintptr_t)15) + 16u * c);
         f.xi = c;
     }
