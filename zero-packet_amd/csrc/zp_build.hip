@@ -489,20 +489,21 @@ __device__ int run_chain(BView<P>& v, const uint8_t ZB_LDSP* stage, uint32_t shi
 }
 
 #define ZB_KATTR __launch_bounds__(64 * ZB_WAVES) __attribute__((amdgpu_waves_per_eu(ZB_WPE)))
-__global__ void ZB_KATTR
-zp_build_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs,
-                const uint32_t* __restrict__ lens, uint64_t n, const zp_build_op* __restrict__ ops,
-                const uint32_t* __restrict__ op_start, const uint8_t* __restrict__ data,
-                zp_build_result* __restrict__ results, int pending_only) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds_all[ZB_WAVES * ZB_F][ZB_LDS];
-    __shared__ __attribute__((aligned(16))) zp_build_op lds_ops[ZB_WAVES * ZB_F][ZB_OPS];
-    // A group of ZB_G lanes builds one frame; the groups of a wave run side
-    // by side (same instructions for same-shaped chains).
-    const int lane = threadIdx.x & (ZB_G - 1);
-    const int slot = threadIdx.x / ZB_G;
-    const uint64_t i = (uint64_t)blockIdx.x * ZB_WAVES * ZB_F + slot;
-    if (i >= n) return;                              // whole group
-    if (pending_only && results[i].err != ZB_PENDING) return;   // done by the lane path
+#ifndef ZB_SCAN
+#define ZB_SCAN 16             // 64-frame spans scanned per wave of the pending pass
+#endif
+
+// Frame i on a group of ZB_G lanes (slot = the group's LDS slot).
+__device__ __forceinline__ void build_frame(uint64_t i, int slot, int lane,
+                                            uint8_t* __restrict__ arena,
+                                            const uint64_t* __restrict__ offs,
+                                            const uint32_t* __restrict__ lens,
+                                            const zp_build_op* __restrict__ ops,
+                                            const uint32_t* __restrict__ op_start,
+                                            const uint8_t* __restrict__ data,
+                                            zp_build_result* __restrict__ results,
+                                            uint8_t (*lds_all)[ZB_LDS],
+                                            zp_build_op (*lds_ops)[ZB_OPS]) {
     const uint32_t len = lens[i];
     uint8_t* const g = arena + offs[i];
     const uint32_t o0 = op_start[i], o1 = op_start[i + 1];
@@ -560,6 +561,43 @@ zp_build_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs,
         r.ops_done = (uint8_t)(done > 255 ? 255 : done);
         r.reserved = 0;
         results[i] = r;
+    }
+}
+
+// The pending pass: the frames the lane path left marked ZB_PENDING. Each
+// wave scans ZB_SCAN spans of 64 results (one ballot per span) and builds the
+// pending ones ZB_F at a time, a lane group per frame; the groups of a wave
+// run side by side (same instructions for same-shaped chains). A small grid:
+// with nothing pending the pass is one read of the results.
+__global__ void ZB_KATTR
+zp_build_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs,
+                const uint32_t* __restrict__ lens, uint64_t n, const zp_build_op* __restrict__ ops,
+                const uint32_t* __restrict__ op_start, const uint8_t* __restrict__ data,
+                zp_build_result* __restrict__ results) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds_all[ZB_WAVES * ZB_F][ZB_LDS];
+    __shared__ __attribute__((aligned(16))) zp_build_op lds_ops[ZB_WAVES * ZB_F][ZB_OPS];
+    const int w = threadIdx.x >> 6, l64 = threadIdx.x & 63;
+    const int g = l64 / ZB_G, lane = l64 & (ZB_G - 1);
+    const int slot = w * ZB_F + g;
+    for (uint32_t k = 0; k < ZB_SCAN; ++k) {
+        const uint64_t base = (((uint64_t)blockIdx.x * ZB_WAVES + w) * ZB_SCAN + k) * 64;
+        if (base >= n) break;                                      // wave-uniform
+        const uint64_t idx = base + l64;
+        uint64_t m = __ballot(idx < n && results[idx].err == ZB_PENDING);
+        while (m) {                                                // wave-uniform
+            // group q takes the q-th lowest pending frame of the span
+            int bit = -1;
+#pragma unroll
+            for (int q = 0; q < ZB_F; ++q) {
+                const int b = m ? __builtin_ctzll(m) : -1;
+                if (q == g) bit = b;
+                m &= m - 1;                                        // m == 0 stays 0
+            }
+            if (bit >= 0)
+                build_frame(base + (uint64_t)bit, slot, lane, arena, offs, lens, ops, op_start,
+                            data, results, lds_all, lds_ops);
+            wave_sync();                                           // slot reused next round
+        }
     }
 }
 
@@ -780,7 +818,7 @@ extern "C" int zp_build_batch_device(uint8_t* arena, const uint64_t* offs, const
         snprintf(zp__errbuf(), 256, "zp_build_batch_device: null pointer");
         return -1;
     }
-    const uint64_t per_block = (uint64_t)ZB_WAVES * ZB_F;
+    const uint64_t per_block = (uint64_t)ZB_WAVES * ZB_SCAN * 64;   // pending pass
     const uint64_t blocks = (n + per_block - 1) / per_block;
     const uint64_t fast_blocks = (n + 63) / 64;
     if (blocks > 0x7FFFFFFFull || fast_blocks > 0x7FFFFFFFull) {
@@ -799,7 +837,7 @@ extern "C" int zp_build_batch_device(uint8_t* arena, const uint64_t* offs, const
                        offs, lens, n, ops, op_start, data, res);
 #ifndef ZB_ABL_NO_SECOND   // timing ablation only (tools/build_variants.sh)
     hipLaunchKernelGGL(zp_build_kernel, dim3((unsigned)blocks), dim3(64 * ZB_WAVES), 0, st, arena,
-                       offs, lens, n, ops, op_start, data, res, 1);
+                       offs, lens, n, ops, op_start, data, res);
 #endif
     if (!results) (void)hipFreeAsync(res, st);
     const hipError_t e = hipGetLastError();
