@@ -589,9 +589,18 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
     uint4 q2[2];
     memcpy(q2, &rec, sizeof rec);
     const uint64_t p = s.tile * 64 + lane;
-    uint4* dst = (uint4*)(records + p);
-    dst[0] = q2[0];
-    dst[1] = q2[1];
+#ifdef ZP_ABL_NOREC
+    if (rec.flags == 0xDEADBEEFu)                       // timing ablation: no stores
+#endif
+    {
+        // Nontemporal stores: the records are write-once output. The record
+        // writes, not their 4 % of the bytes, are what makes the kernel
+        // sensitive to the arena's placement (without them every placement
+        // runs in 1.95 ms); nt takes 6-7 % off on every placement (r01).
+        zp_u32x4* dst = (zp_u32x4*)(records + p);
+        __builtin_nontemporal_store(zp_u32x4{q2[0].x, q2[0].y, q2[0].z, q2[0].w}, dst);
+        __builtin_nontemporal_store(zp_u32x4{q2[1].x, q2[1].y, q2[1].z, q2[1].w}, dst + 1);
+    }
     if (inner_ext && (rec.flags & ZP_F_INNER_EXT)) inner_ext[p] = w.inner;
     if (COLS) {
         ViewReader rdr{fv};
