@@ -24,7 +24,7 @@ for s in "$@"; do
     tests)  step gpu_tests 1200 python -m pytest tests -m gpu -q -p no:cacheprovider --timeout 600 ;;
     smoke)  step smoke 300 python __graft_entry__.py smoke ;;
     bench)  step bench 900 python bench.py ;;
-    prof)   step prof 900 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --steps 10 --no-cpu --no-pcie ;;
+    prof)   step prof 900 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --no-pcie ;;
     *) step "step$i" 900 bash -c "$s" ;;
   esac
 done
