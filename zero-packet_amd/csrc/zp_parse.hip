@@ -55,10 +55,16 @@
 #ifndef ZP_K
 #define ZP_K 1               // consecutive tiles per wave
 #endif
-// Timing-only ablations (tools/build_variants.sh); never set in the product:
+// Timing-only ablations and diagnostics (tools/build_variants.sh,
+// tools/alloc_probe.py --no-check); never set in the product:
 //   ZP_ABL_FAKE_WALK  replace the walk by "pending L4 at offset 42"
 //   ZP_ABL_STREAM_OFF skip the stream loads
+//   ZP_ABL_NOSCAN     no per-item wave scan (zp_stream.h)
+//   ZP_ABL_EXTRA=n    n extra dependent VALU per stream item (zp_stream.h)
+//   ZP_ABL_NO_IPSUM / ZP_ABL_NO_PSEUDO / ZP_ABL_NO_L4HDR  skip one header sum
+//   ZP_ABL_NOREC      no record stores
 //   ZP_STAMPS         per-wave phase timestamps (tools/stamps.py)
+//   ZP_DBG_FBCOUNT    count past-window chunk loads (tools/fbcount.py)
 
 static __thread char g_last_error[256];
 
