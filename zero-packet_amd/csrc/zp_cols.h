@@ -13,18 +13,30 @@ struct ColPtrs {
     uint8_t* p[ZP_COL_COUNT];
 };
 
-template <class R>
-__device__ __forceinline__ uint32_t rd16(R& rd, uint32_t x) { return (rd(x) << 8) | rd(x + 1); }
-template <class R>
-__device__ __forceinline__ uint32_t rd32(R& rd, uint32_t x) {
-    return (rd16(rd, x) << 16) | rd16(rd, x + 2);
-}
+// A reader R gives frame byte x as rd(x), and bytes [x, x + 4) as one
+// little-endian dword rd.le4(x) when rd.has4(x) (all four staged: two dword
+// reads and a v_alignbyte instead of four byte reads).
+
 // n bytes [x, x + n) packed little-endian (n <= 4): memory order preserved.
 template <class R>
 __device__ __forceinline__ uint32_t rd_le(R& rd, uint32_t x, int n) {
+    if (rd.has4(x)) {
+        const uint32_t v = rd.le4(x);
+        return n >= 4 ? v : v & ((1u << (8 * n)) - 1u);
+    }
     uint32_t v = 0;
     for (int k = 0; k < n; ++k) v |= rd(x + k) << (8 * k);
     return v;
+}
+// Big-endian fields.
+template <class R>
+__device__ __forceinline__ uint32_t rd16(R& rd, uint32_t x) {
+    const uint32_t v = rd_le(rd, x, 2);
+    return ((v & 0xFFu) << 8) | (v >> 8);
+}
+template <class R>
+__device__ __forceinline__ uint32_t rd32(R& rd, uint32_t x) {
+    return __builtin_bswap32(rd_le(rd, x, 4));
 }
 
 template <typename T>

@@ -63,9 +63,19 @@ __device__ __forceinline__ uint32_t hb(Hdr& h, uint32_t x) {
     const uint32_t w = d == 0 ? h.xc.x : d == 1 ? h.xc.y : d == 2 ? h.xc.z : h.xc.w;
     return (w >> (8 * (y & 3))) & 0xFFu;
 }
+// Dword z (4-aligned, from A & ~15) of the staged window.
+__device__ __forceinline__ uint32_t hdw(const Hdr& h, uint32_t z) {
+    return *(const uint32_t*)(h.win + (z >> 4) * 16 * FX_BLOCK + (z & 15));
+}
 struct HdrReader {
     Hdr& h;
     __device__ __forceinline__ uint32_t operator()(uint32_t x) { return hb(h, x); }
+    __device__ __forceinline__ bool has4(uint32_t x) const { return x + 3 < h.wlen; }
+    __device__ __forceinline__ uint32_t le4(uint32_t x) const {
+        const uint32_t y = x + h.shift, z = y & ~3u;
+        const uint32_t lo = hdw(h, z), hi = (y & 3) ? hdw(h, z + 4) : 0u;
+        return __builtin_amdgcn_alignbyte(hi, lo, y & 3);
+    }
 };
 
 __global__ void __launch_bounds__(FX_BLOCK)

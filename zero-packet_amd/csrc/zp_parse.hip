@@ -197,7 +197,7 @@ __device__ __forceinline__ void chunk_vb(uint4 v, int l, int h, uint32_t& V, uin
 // V and B over frame bytes [lo, hi) (both <= len): window chunks from LDS,
 // chunks past the window through the fallback cache.
 template <bool WANT_B>
-__device__ void sum_vb(FrameView& f, uint32_t lo, uint32_t hi, uint32_t& V, uint32_t& B) {
+__device__ __forceinline__ void sum_vb(FrameView& f, uint32_t lo, uint32_t hi, uint32_t& V, uint32_t& B) {
     V = 0;
     B = 0;
     const uint32_t h1 = hi < f.wlen ? hi : f.wlen;
@@ -265,7 +265,7 @@ __device__ __forceinline__ uint32_t sum_to(FrameView& f, uint32_t x) {
 // bytes [lo, hi), hi - lo even: with E/O the byte sums at even/odd ARENA
 // addresses, V = E + 256*O and B = E + O, so O = (V - B) / 255 exactly; the
 // words start at an even address iff A + lo is even.
-__device__ uint32_t sumW_exact(FrameView& f, uint32_t lo, uint32_t hi) {
+__device__ __forceinline__ uint32_t sumW_exact(FrameView& f, uint32_t lo, uint32_t hi) {
 #ifndef ZP_SUMW_BYTES
     uint32_t V, B;
     sum_vb<true>(f, lo, hi, V, B);
@@ -334,7 +334,7 @@ struct Walk {
 
 // Extension-header walk (headers.rs:51-213). Returns 0 or a zp_err.
 // pos = IPv6 payload start; outputs slot offsets relative to pos.
-__device__ int ext_walk(FrameView& f, uint32_t pos, uint32_t nh,
+__device__ __forceinline__ int ext_walk(FrameView& f, uint32_t pos, uint32_t nh,
                         uint32_t* present, uint16_t off[6], uint32_t* total,
                         uint32_t* final_nh) {
     uint32_t pres = 0, tot = 0, fin = 0;
@@ -392,7 +392,7 @@ __device__ int ext_walk(FrameView& f, uint32_t pos, uint32_t nh,
     return 0;
 }
 
-__device__ void walk_frame(FrameView& f, Walk& w) {
+__device__ __forceinline__ void walk_frame(FrameView& f, Walk& w) {
     zp_record& r = w.rec;
     w.pending = 0; w.acc = 0; w.l4 = 0; w.v6 = 0;
     const uint32_t len = f.len;
@@ -535,6 +535,12 @@ struct ViewReader {
             return (win_dw(f, y >> 2) >> ((y & 3) * 8)) & 0xFFu;
         }
         return *(const ZP_GLOBAL uint8_t*)((uintptr_t)f.g + x);
+    }
+    __device__ __forceinline__ bool has4(uint32_t x) const { return x + 3 < f.wlen; }
+    __device__ __forceinline__ uint32_t le4(uint32_t x) const {
+        const uint32_t y = x + f.shift, d = y >> 2;
+        const uint32_t lo = win_dw(f, d), hi = (y & 3) ? win_dw(f, d + 1) : 0u;
+        return __builtin_amdgcn_alignbyte(hi, lo, y & 3);
     }
 };
 
