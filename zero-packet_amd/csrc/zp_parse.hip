@@ -466,26 +466,30 @@ __device__ __forceinline__ void walk_frame(FrameView& f, Walk& w) {
                     }
                 }
                 const uint32_t rem = len - pp;                        // parse_protocol :111-140
-                if (proto == 6) {
-                    if (rem < 20) { err = ZP_ERR_TCP_TOO_SHORT; goto done; }
-                    const uint32_t t = rd16(f, pp + 12);
-                    if ((t >> 12) * 4 < 20) { err = ZP_ERR_TCP_DATA_OFFSET; goto done; }
-                    if ((t & 0xFF) == 0) { err = ZP_ERR_TCP_FLAGS; goto done; }
-                    r.flags |= ZP_F_TCP;
-                } else if (proto == 17) {
-                    if (rem < 8) { err = ZP_ERR_UDP_TOO_SHORT; goto done; }
-                    if (rd16(f, pp + 4) != rem) { err = ZP_ERR_UDP_LENGTH; goto done; }
-                    r.flags |= ZP_F_UDP;
-                } else if (proto == 1) {
-                    if (rem < 8) { err = ZP_ERR_ICMP_TOO_SHORT; goto done; }
-                    const uint32_t t = rd16(f, pp);
-                    if (!icmpv4_type_ok(t >> 8)) { err = ZP_ERR_ICMPV4_TYPE; goto done; }
-                    if ((t & 0xFF) > 15) { err = ZP_ERR_ICMPV4_CODE; goto done; }
-                    r.flags |= ZP_F_ICMPV4;
-                } else if (proto == 58) {
-                    if (rem < 8) { err = ZP_ERR_ICMP_TOO_SHORT; goto done; }
-                    if (!icmpv6_type_ok(rd8(f, pp))) { err = ZP_ERR_ICMPV6_TYPE; goto done; }
-                    r.flags |= ZP_F_ICMPV6;
+                const bool tcp = proto == 6, udp = proto == 17, ic4 = proto == 1;
+                if (tcp || udp || ic4 || proto == 58) {
+                    // One code path for the four L4 readers (no divergent
+                    // duplicate per type): each reads one 16-bit word, at
+                    // +12 (TCP data offset/flags), +4 (UDP length) or +0
+                    // (ICMP type/code); the checks and error codes per type
+                    // are those of tcp.rs:141-147 / parser.rs:237-247,
+                    // udp.rs:103-107 / parser.rs:258-263, icmpv4.rs:92-97 /
+                    // parser.rs:273-283, icmpv6.rs:89-94 / parser.rs:293-299.
+                    if (rem < (tcp ? 20u : 8u)) {
+                        err = tcp ? ZP_ERR_TCP_TOO_SHORT
+                                  : udp ? ZP_ERR_UDP_TOO_SHORT : ZP_ERR_ICMP_TOO_SHORT;
+                        goto done;
+                    }
+                    const uint32_t t = rd16(f, pp + (tcp ? 12u : udp ? 4u : 0u));
+                    int e;
+                    if (tcp) e = (t >> 12) * 4 < 20 ? ZP_ERR_TCP_DATA_OFFSET
+                               : (t & 0xFF) == 0 ? ZP_ERR_TCP_FLAGS : 0;
+                    else if (udp) e = t != rem ? ZP_ERR_UDP_LENGTH : 0;
+                    else if (ic4) e = !icmpv4_type_ok(t >> 8) ? ZP_ERR_ICMPV4_TYPE
+                                    : (t & 0xFF) > 15 ? ZP_ERR_ICMPV4_CODE : 0;
+                    else e = !icmpv6_type_ok(t >> 8) ? ZP_ERR_ICMPV6_TYPE : 0;
+                    if (e) { err = e; goto done; }
+                    r.flags |= tcp ? ZP_F_TCP : udp ? ZP_F_UDP : ic4 ? ZP_F_ICMPV4 : ZP_F_ICMPV6;
                 } else if (proto == 4 || proto == 41) {               // IP-in-IP recursion
                     v4 = proto == 4;
                     pos = pp;
@@ -496,7 +500,7 @@ __device__ __forceinline__ void walk_frame(FrameView& f, Walk& w) {
                 // Pseudo-header of the innermost IP only (outer levels of an
                 // IP-in-IP chain never need one): parser.rs:316-333 (IPv4;
                 // none for ICMPv4), parser.rs:341-361 (IPv6, final next header).
-// One pseudo-header sum for both IP versions (the address range differs,
+                // One pseudo-header sum for both IP versions (the address range differs,
                 // the code does not: no divergent duplicate).
 #ifdef ZP_ABL_NO_PSEUDO
                 const uint32_t ps = 0;                                // timing ablation only
