@@ -304,3 +304,30 @@ def test_full_size_properties(zp, config, n):
     r3, _ = zp.batch.parse_batch(arena, offs, lens)
     torch.cuda.synchronize()
     assert torch.equal(r3[:, 4], want_err)
+
+
+# ---- maximum size: the whole BASELINE config 5 on one GPU ------------------
+
+def test_max_size_full_imix_one_gpu(zp):
+    """All 268,435,456 IMIX frames of config 5 (95 GB, arena offsets past
+    2^36, 4M workgroups) in one launch: every frame accepted, 4,000 sampled
+    frames (the last 1,000 among them) byte-exact vs the oracle."""
+    torch.cuda.empty_cache()                 # earlier tests' cached blocks
+    free, _ = torch.cuda.mem_get_info()
+    if free < 120e9:
+        pytest.skip(f"needs ~110 GB of free HBM, {free / 1e9:.0f} GB free")
+    n = 256 << 20
+    arena, offs, lens = zp.batch.generate("c5", n, device=dev())
+    assert int(offs[-1].item()) > (1 << 36)
+    rec, ext = zp.batch.parse_batch(arena, offs, lens)
+    assert int((rec[:, 4] != 0).sum()) == 0
+    g = torch.Generator(device=arena.device).manual_seed(5)
+    idx = torch.cat([torch.randint(0, n, (3000,), device=arena.device, generator=g),
+                     torch.arange(n - 1000, n, device=arena.device)])
+    so, sl = offs[idx].cpu().numpy(), lens[idx].cpu().numpy()
+    frames = [arena[int(o):int(o) + int(l)].cpu().numpy().tobytes() for o, l in zip(so, sl)]
+    del arena
+    sa, sof, sle = pack(frames)
+    want, wext = orc.parse_batch(sa, sof, sle)
+    got, gext = zp.batch.records_to_numpy(rec[idx], ext[idx])
+    assert_same(got, gext, want, wext)
