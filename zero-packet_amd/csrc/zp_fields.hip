@@ -23,7 +23,9 @@
 
 extern "C" char* zp__errbuf(void);
 
-#define FX_WIN 128                       // staged bytes per frame (from A & ~15)
+#ifndef FX_WIN
+#define FX_WIN 160                       // staged bytes per frame (from A & ~15): covers c4 headers
+#endif
 #define FX_CH (FX_WIN / 16)
 #define FX_BLOCK 256
 
@@ -126,12 +128,18 @@ zp_columns_kernel(const uint8_t* __restrict__ arena, const uint64_t* __restrict_
         const uint32_t a_lo = (uint32_t)a0, a_hi = (uint32_t)(a0 >> 32);
 #pragma unroll
         for (uint32_t q = 0; q < 8; ++q) {
-            const uint32_t f = 8 * q + (lane >> 3), ch = lane & 7;
+            const uint32_t f = 8 * q + (lane >> 3);
             const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(f << 2), (int)a_lo);
             const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(f << 2), (int)a_hi);
             const uint32_t nc = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(f << 2), (int)nch);
-            if (ch < nc)
-                win[ch * FX_BLOCK + wbase + f] = fx_ld16((((uintptr_t)hi << 32) | lo) + 16u * ch);
+            // windows past 128 B: further rounds of 8 chunks per frame
+#pragma unroll
+            for (uint32_t g = 0; g < (FX_CH + 7) / 8; ++g) {
+                const uint32_t ch = 8 * g + (lane & 7);
+                if (ch < nc && ch < FX_CH)
+                    win[ch * FX_BLOCK + wbase + f] =
+                        fx_ld16((((uintptr_t)hi << 32) | lo) + 16u * ch);
+            }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
