@@ -529,17 +529,12 @@ done:
 }
 
 // Byte reader over a FrameView for the fused column views (zp_cols.h): the
-// LDS window, then plain global byte loads (the walk's one-chunk cache here
-// makes the fused kernel spill to scratch).
+// LDS window, then the walk's one-chunk cache past it (c4 fused −4 % against
+// plain global byte loads; no stack frame since the walk helpers are
+// force-inlined).
 struct ViewReader {
-    const FrameView& f;
-    __device__ __forceinline__ uint32_t operator()(uint32_t x) {
-        if (x < f.wlen) {
-            const uint32_t y = x + f.shift;
-            return (win_dw(f, y >> 2) >> ((y & 3) * 8)) & 0xFFu;
-        }
-        return *(const ZP_GLOBAL uint8_t*)((uintptr_t)f.g + x);
-    }
+    FrameView& f;
+    __device__ __forceinline__ uint32_t operator()(uint32_t x) { return rd8(f, x); }
     __device__ __forceinline__ bool has4(uint32_t x) const { return x + 3 < f.wlen; }
     __device__ __forceinline__ uint32_t le4(uint32_t x) const {
         const uint32_t y = x + f.shift, d = y >> 2;
