@@ -161,6 +161,11 @@ const char* zp_last_error(void);
  * overlaps and any order are allowed); the fast path is taken for the common
  * packed, increasing layout. `inner_ext` may be NULL. Returns 0 on success or
  * a negative value if the launch failed (see zp_last_error()).
+ * Precondition (not checked on the device: the descriptors live in HBM and the
+ * call does not synchronise): offs[i] + lens[i] <= the arena's size for every
+ * i. A descriptor past the arena reads past the allocation and faults the
+ * GPU. The Python wrapper (batch.parse_batch) checks this with one device
+ * reduction unless told not to.
  */
 int zp_parse_batch_device(const uint8_t* arena, const uint64_t* offs,
                           const uint32_t* lens, uint64_t n,
@@ -170,7 +175,10 @@ int zp_parse_batch_device(const uint8_t* arena, const uint64_t* offs,
 /* Host-buffer convenience path: the frames, descriptors and outputs live in
  * host memory (a NIC ring / raw socket buffer). Stages through pinned buffers
  * and overlaps H2D copy, parse and D2H copy in chunks on `ctx`'s streams.
- * Synchronous. Returns 0 on success, negative on HIP failure. */
+ * Synchronous. Returns 0 on success, negative on HIP failure.
+ * A zp_ctx owns pinned staging buffers, device buffers and streams: it must
+ * not be used by two host threads at once (one context per thread, or a
+ * lock around every call that takes it, as the Python facade does). */
 typedef struct zp_ctx zp_ctx;
 zp_ctx* zp_ctx_create(int device, uint64_t chunk_bytes);
 void    zp_ctx_destroy(zp_ctx* ctx);

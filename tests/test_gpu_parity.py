@@ -331,3 +331,56 @@ def test_max_size_full_imix_one_gpu(zp):
     want, wext = orc.parse_batch(sa, sof, sle)
     got, gext = zp.batch.records_to_numpy(rec[idx], ext[idx])
     assert_same(got, gext, want, wext)
+
+
+# ---- API guards ------------------------------------------------------------
+
+def test_descriptor_bounds_refused(zp):
+    """Frames past the arena, negative offsets/lengths and mis-shaped outputs
+    are refused before any launch (the kernel does not check descriptors)."""
+    d = dev()
+    a = torch.zeros(1024, dtype=torch.uint8, device=d)
+    o = torch.tensor([0, 512], dtype=torch.int64, device=d)
+    good = torch.tensor([64, 512], dtype=torch.int32, device=d)
+    zp.batch.parse_batch(a, o, good)                              # ends exactly at the arena end
+    for lens in ([64, 513], [64, -1]):
+        with pytest.raises(ValueError):
+            zp.batch.parse_batch(a, o, torch.tensor(lens, dtype=torch.int32, device=d))
+    with pytest.raises(ValueError):
+        zp.batch.parse_batch(a, torch.tensor([0, -64], dtype=torch.int64, device=d), good)
+    with pytest.raises(ValueError):
+        zp.batch.parse_batch(a, o, good, records=torch.empty((2, 16), dtype=torch.uint8, device=d))
+    with pytest.raises(ValueError):
+        zp.batch.parse_batch(a, o, good, inner_ext=torch.empty((2, 12), dtype=torch.uint8))
+    with pytest.raises(ValueError):
+        zp.columns.parse_with_columns(a, o, torch.tensor([64, 600], dtype=torch.int32, device=d))
+    r, _ = zp.batch.parse_batch(a, o, good)
+    with pytest.raises(ValueError):
+        zp.columns.extract(a, o, torch.tensor([2048, 64], dtype=torch.int32, device=d), r)
+
+
+def test_parse_one_threads(zp, golden):
+    """PacketParser.parse from several threads at once (one shared zp_ctx
+    behind a lock): every thread gets its own frame's result."""
+    import threading
+    frames = [bytes.fromhex(fx["bytes"]) for fx in golden["fixtures"]]
+
+    def result(f):
+        try:
+            return zp.parser.PacketParser.parse(f).debug()
+        except zp.parser.ZeroPacketError as e:     # Err(&str): same string each time
+            return repr(e)
+    want = [result(f) for f in frames]
+    bad = []
+
+    def worker(k):
+        for it in range(40):
+            i = (k + it) % len(frames)
+            if result(frames[i]) != want[i]:
+                bad.append((k, it, i))
+    ts = [threading.Thread(target=worker, args=(k,)) for k in range(8)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not bad, bad[:5]

@@ -22,12 +22,12 @@ zp = importlib.import_module("zero-packet_amd")
 def timeit(arena, offs, lens, records, inner, steps, base=None):
     s = torch.cuda.current_stream()
     for _ in range(3):
-        zp.batch.parse_batch(arena, offs, lens, records, inner)
+        zp.batch.parse_batch(arena, offs, lens, records, inner, check=False)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(steps)]
     for a, b in ev:
         a.record(s)
-        zp.batch.parse_batch(arena, offs, lens, records, inner)
+        zp.batch.parse_batch(arena, offs, lens, records, inner, check=False)
         b.record(s)
     torch.cuda.synchronize()
     assert int((records[:, 4] != 0).sum().item()) == 0

@@ -148,12 +148,12 @@ def main():
             print(f"{cfg} {name:>12}: {med:8.3f} ms  {nbytes / med / 1e6:7.0f} GB/s  "
                   f"{n / med / 1e3:8.0f} Mpkt/s  (min {min(ms):.3f})", flush=True)
         if args.columns:
-            zp.batch.parse_batch(arena, offs, lens, rec, ext)
+            zp.batch.parse_batch(arena, offs, lens, rec, ext, check=False)
             for label, names in (("all", zp.columns.NAMES),
                                  ("5tuple", ["src_addr", "dest_addr", "protocol", "src_port",
                                              "dest_port"])):
                 out = zp.columns.extract(arena, offs, lens, rec, names=names)
-                ms = time_launches(lambda: zp.columns.extract(arena, offs, lens, rec, names=names,
+                ms = time_launches(lambda: zp.columns.extract(arena, offs, lens, rec, names=names, check=False,
                                                               out=out), args.reps * args.rounds)
                 med = float(np.median(ms))
                 wbytes = n * sum(zp.columns.width(c) for c in names)
@@ -163,7 +163,7 @@ def main():
                       f"  (write+read {(wbytes + rbytes) / med / 1e6:6.0f} GB/s)  "
                       f"{n / med / 1e3:8.0f} Mpkt/s", flush=True)
                 ms = time_launches(lambda: zp.columns.parse_with_columns(
-                    arena, offs, lens, names=names, records=rec, inner_ext=ext, out=out),
+                    arena, offs, lens, names=names, records=rec, inner_ext=ext, out=out, check=False),
                     args.reps * args.rounds)
                 med = float(np.median(ms))
                 print(f"{cfg} fused parse+columns[{label}]: {med:8.3f} ms  "

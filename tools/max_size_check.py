@@ -29,11 +29,11 @@ def main():
     print(f"generated {n} frames, {nbytes / 1e9:.1f} GB in {time.time() - t0:.1f} s", flush=True)
     rec = torch.empty((n, 32), dtype=torch.uint8, device=d)
     ext = torch.zeros((n, 12), dtype=torch.uint8, device=d)
-    zp.batch.parse_batch(arena, offs, lens, rec, ext)
+    zp.batch.parse_batch(arena, offs, lens, rec, ext, check=False)
     s = torch.cuda.current_stream()
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     ev[0].record(s)
-    zp.batch.parse_batch(arena, offs, lens, rec, ext)
+    zp.batch.parse_batch(arena, offs, lens, rec, ext, check=False)
     ev[1].record(s)
     torch.cuda.synchronize()
     ms = ev[0].elapsed_time(ev[1])

@@ -31,17 +31,55 @@ def _need_cuda(*ts):
             raise RuntimeError("zero-packet_amd batch API needs device tensors (no CPU fallback)")
 
 
-def parse_batch(arena, offs, lens, records=None, inner_ext=None, stream=None):
-    """Parses every frame; returns (records, inner_ext) as uint8 device tensors."""
+def check_batch(arena, offs, lens, outs=(), bounds=True):
+    """Validates a device batch before a kernel reads it: dtypes, shapes,
+    contiguity and device of every tensor, and (bounds=True) that every frame
+    lies inside the arena: 0 <= offs[i], 0 <= lens[i], offs[i] + lens[i] <=
+    arena.numel(). The kernels do not check descriptors on the device (a frame
+    past the arena faults the GPU), so this is the Python API's guard; it
+    costs one device reduction and one synchronisation. `outs` holds
+    (tensor, row_bytes) pairs of outputs ([n, row_bytes] uint8, or any
+    contiguous tensor of n * row_bytes bytes)."""
     _need_cuda(arena, offs, lens)
     n = offs.numel()
-    assert lens.numel() == n and offs.dtype == torch.int64 and lens.dtype == torch.int32
-    assert arena.dtype == torch.uint8 and arena.is_contiguous()
+    if arena.dtype != torch.uint8 or arena.dim() != 1 or not arena.is_contiguous():
+        raise ValueError("arena must be a contiguous 1-D uint8 tensor")
+    if offs.dtype != torch.int64 or lens.dtype != torch.int32:
+        raise ValueError("offs must be int64 and lens int32")
+    if lens.numel() != n or not offs.is_contiguous() or not lens.is_contiguous():
+        raise ValueError("offs and lens must be contiguous with the same length")
     dev = arena.device
-    if records is None:
+    for t, row in outs:
+        if t is None:
+            continue
+        if not t.is_cuda or t.device != dev:
+            raise ValueError(f"output tensor on {t.device}, arena on {dev}")
+        if not t.is_contiguous() or t.numel() * t.element_size() != n * row:
+            raise ValueError(f"output tensor must be contiguous with {n} x {row} bytes")
+    for t in (offs, lens):
+        if t.device != dev:
+            raise ValueError(f"descriptor tensor on {t.device}, arena on {dev}")
+    if bounds and n:
+        lo = torch.minimum(offs.min(), lens.min().to(torch.int64))
+        hi = (offs + lens.to(torch.int64)).max()
+        lo, hi = torch.stack([lo, hi]).tolist()
+        if lo < 0:
+            raise ValueError("negative frame offset or length")
+        if hi > arena.numel():
+            raise ValueError(f"frame ends at byte {hi}, past the arena ({arena.numel()} bytes)")
+
+
+def parse_batch(arena, offs, lens, records=None, inner_ext=None, stream=None, check=True):
+    """Parses every frame; returns (records, inner_ext) as uint8 device tensors.
+    check=False skips the descriptor bounds reduction (check_batch) for callers
+    that validated the batch already; shapes and devices are always checked."""
+    n = offs.numel()
+    dev = arena.device
+    if records is None and arena.is_cuda:
         records = torch.empty((n, 32), dtype=torch.uint8, device=dev)
-    if inner_ext is None:
+    if inner_ext is None and arena.is_cuda:
         inner_ext = torch.zeros((n, 12), dtype=torch.uint8, device=dev)
+    check_batch(arena, offs, lens, ((records, 32), (inner_ext, 12)), bounds=check)
     s = ctypes.c_void_p(stream) if stream is not None else _stream_ptr(dev)
     rc = _lib.hip().zp_parse_batch_device(arena.data_ptr(), offs.data_ptr(), lens.data_ptr(), n,
                                           records.data_ptr(), inner_ext.data_ptr(), s)

@@ -14,6 +14,7 @@ import numpy as np
 import torch
 
 from . import _lib
+from .batch import check_batch
 
 # (name, torch dtype, elements per frame) in zp_col order.
 COLUMNS = [
@@ -46,14 +47,15 @@ def _alloc(name, n, device):
     return torch.empty((n, k) if k > 1 else (n,), dtype=dt, device=device)
 
 
-def extract(arena, offs, lens, records, names=None, out=None, stream=None):
+def extract(arena, offs, lens, records, names=None, out=None, stream=None, check=True):
     """Fills the requested columns (default: all) on the device; returns
-    {name: tensor}. `out` may hold preallocated tensors."""
+    {name: tensor}. `out` may hold preallocated tensors. check: as in
+    batch.parse_batch (descriptor bounds reduction)."""
     for t in (arena, offs, lens, records):
         if not t.is_cuda:
             raise RuntimeError("columns.extract needs device tensors (no CPU fallback)")
     n = offs.numel()
-    assert lens.numel() == n and records.shape[0] == n
+    check_batch(arena, offs, lens, ((records, 32),), bounds=check)
     names = list(names) if names is not None else NAMES
     out = dict(out or {})
     ptrs = (ctypes.c_void_p * len(COLUMNS))()
@@ -72,7 +74,7 @@ def extract(arena, offs, lens, records, names=None, out=None, stream=None):
 
 
 def parse_with_columns(arena, offs, lens, names=None, records=None, inner_ext=None, out=None,
-                       stream=None):
+                       stream=None, check=True):
     """zp_parse_batch_columns_device: records and the requested columns in one
     pass over the frames. Returns (records, inner_ext, {name: tensor})."""
     for t in (arena, offs, lens):
@@ -91,6 +93,8 @@ def parse_with_columns(arena, offs, lens, names=None, records=None, inner_ext=No
         if name not in out:
             out[name] = _alloc(name, n, d)
         ptrs[INDEX[name]] = out[name].data_ptr()
+    check_batch(arena, offs, lens, [(records, 32), (inner_ext, 12)] +
+                [(out[k], width(k)) for k in names], bounds=check)
     s = ctypes.c_void_p(stream) if stream is not None else \
         ctypes.c_void_p(torch.cuda.current_stream(d).cuda_stream)
     rc = _lib.hip().zp_parse_batch_columns_device(arena.data_ptr(), offs.data_ptr(),

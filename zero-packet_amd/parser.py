@@ -11,6 +11,7 @@ PacketParser.parse(frame) parses through the GPU (zp_parse_one); batches go
 through zero-packet_amd.batch. There is no CPU parse path in this package.
 """
 import ctypes
+import threading
 
 import numpy as np
 
@@ -448,8 +449,12 @@ class PacketParser:
         rec = np.zeros(1, RECORD_DTYPE)
         ext = np.zeros(1, EXT_DTYPE)
         buf = ctypes.create_string_buffer(frame, len(frame) or 1)
-        rc = _lib.hip().zp_parse_one(_default_ctx(), ctypes.addressof(buf), len(frame),
-                                     rec.ctypes.data, ext.ctypes.data)
+        # The shared zp_ctx (pinned staging, device buffers, streams) serves one
+        # call at a time; ctypes releases the GIL, so callers on other threads
+        # wait here (the reference's parse is pure and thread-safe).
+        with _CTX_LOCK:
+            rc = _lib.hip().zp_parse_one(_default_ctx(), ctypes.addressof(buf), len(frame),
+                                         rec.ctypes.data, ext.ctypes.data)
         _lib.check(rc, "zp_parse_one")
         return cls.from_record(frame, rec[0], ext[0])
 
@@ -463,9 +468,11 @@ def _lib_available():
 
 
 _CTX = None
+_CTX_LOCK = threading.Lock()
 
 
 def _default_ctx():
+    """The module's zp_ctx; callers hold _CTX_LOCK."""
     global _CTX
     if _CTX is None:
         _CTX = _lib.hip().zp_ctx_create(0, 0)
