@@ -231,6 +231,10 @@ def main():
         if not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(zp, arena, offs, lens, args.cpu_sample,
                                                args.cpu_seconds)
+            # vs_baseline stays null: BASELINE.md has no published number for
+            # this metric. The ratio to the CPU leg of this run is reported
+            # beside it instead.
+            out["vs_cpu_baseline"] = round(out["value"] / out["cpu_baseline"]["value"], 1)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
