@@ -108,7 +108,7 @@ def pcie_inclusive(zp, arena, offs, lens, sample_pkts):
     end = int(o[-1] + ln[-1])
     host = torch.empty(end, dtype=torch.uint8).pin_memory()
     host.copy_(arena[:end])
-    recs = torch.empty((m, 32), dtype=torch.uint8).pin_memory()
+    recs = torch.empty((m, 16), dtype=torch.uint8).pin_memory()
     lib = zp._lib.hip()
     ctx = lib.zp_ctx_create(torch.cuda.current_device(), 256 << 20)
     args = (ctx, host.data_ptr(), end, o.ctypes.data, ln.ctypes.data, m, recs.data_ptr(), None)
@@ -163,8 +163,8 @@ def main():
     n = args.packets or DEFAULT_PACKETS[args.config]
     t0 = time.perf_counter()
     arena, offs, lens = zp.batch.generate(args.config, n, first=rank * n, device=dev)
-    records = torch.empty((n, 32), dtype=torch.uint8, device=dev)
-    inner = torch.zeros((n, 12), dtype=torch.uint8, device=dev)
+    records = torch.empty((n, 16), dtype=torch.uint8, device=dev)
+    ext = torch.empty((2, n, 16), dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
     total_bytes = int(lens.to(torch.int64).sum().item())
     log(f"[rank {rank}] generated {n} frames, {total_bytes/1e9:.2f} GB in "
@@ -172,12 +172,12 @@ def main():
 
     # One checked parse (descriptor bounds, shapes) whatever --warmup is: the
     # rejected-frame check below reads its records.
-    zp.batch.parse_batch(arena, offs, lens, records, inner, check=True)
+    zp.batch.parse_batch(arena, offs, lens, records, ext, check=True)
     torch.cuda.synchronize()
     errs = int((records[:, 4] != 0).sum().item())
     assert errs == 0, f"{errs} frames rejected (generator/kernel mismatch)"
     for _ in range(args.warmup):
-        zp.batch.parse_batch(arena, offs, lens, records, inner, check=False)
+        zp.batch.parse_batch(arena, offs, lens, records, ext, check=False)
     torch.cuda.synchronize()
 
     stream = torch.cuda.current_stream(dev)
@@ -188,7 +188,7 @@ def main():
     t0 = time.perf_counter()
     for k in range(args.steps):
         ev[k][0].record(stream)
-        zp.batch.parse_batch(arena, offs, lens, records, inner, check=False)
+        zp.batch.parse_batch(arena, offs, lens, records, ext, check=False)
         ev[k][1].record(stream)
     torch.cuda.synchronize()
     barrier()

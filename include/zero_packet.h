@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define ZP_ABI_VERSION 1
+#define ZP_ABI_VERSION 2   /* 2: 16-B record, extension chains in the ext side array */
 
 /* ------------------------------------------------------------------------- */
 /* Per-packet parse error codes. One code per DISTINCT reference error string */
@@ -106,18 +106,20 @@ typedef enum zp_err {
 #define ZP_F_INNER_EXT_SLOT(k) (1u << (18 + (k)))  /* inner set             */
 
 /*
- * One parse result, 32 bytes. All offsets are FRAME offsets (bytes from the
- * first byte of the frame) unless stated. When err != ZP_OK the reference
- * returns Err and no PacketParser exists: the record is then all zero except
- * `err`.
+ * One parse result, 16 bytes (one dwordx4 store per frame: the record writes
+ * are the only HBM writes of the parse and the only traffic besides the
+ * frames themselves). All offsets are FRAME offsets (bytes from the first
+ * byte of the frame). When err != ZP_OK the reference returns Err and no
+ * PacketParser exists: the record is then all zero except `err`.
  *
  *  - ethernet/arp/ipv4/ipv6 start at offsets 0 / eth_len / eth_len / eth_len.
- *  - ext_off[k] is relative to the outer IPv6 payload (frame offset
- *    eth_len + 40 + ext_off[k]); ext_len = IPv6Reader::extension_headers_len
- *    (ipv6.rs:141); final_nh = IPv6Reader::final_next_header() (ipv6.rs:219).
- *  - inner_off is the ip_in_ip header; its IPv6 extension offsets (relative to
- *    inner_off + 40) go to the optional zp_ext_offsets side array.
+ *  - final_nh = IPv6Reader::final_next_header() (ipv6.rs:219) of the outer
+ *    IPv6, inner_final_nh that of an ip_in_ip IPv6.
+ *  - inner_off is the ip_in_ip header.
  *  - l4_off is the start of the single tcp/udp/icmpv4/icmpv6 reader.
+ *  - The two Option<ExtensionHeaders> (outer ipv6, ip_in_ip IPv6) go to the
+ *    zp_ext_offsets side array (below); ZP_F_EXT / ZP_F_INNER_EXT and the
+ *    slot bits say which are Some.
  */
 typedef struct zp_record {
     uint32_t flags;
@@ -127,15 +129,24 @@ typedef struct zp_record {
     uint8_t  inner_final_nh; /* ip_in_ip IPv6 final next header            */
     uint32_t inner_off;
     uint32_t l4_off;
-    uint16_t ext_len;
-    uint16_t ext_off[ZP_EXT_SLOTS];
-    uint16_t inner_ext_len;
 } zp_record;
 
-/* Extension offsets of the ip_in_ip IPv6 header (written only when
- * flags & ZP_F_INNER_EXT; relative to the inner IPv6 payload). */
+/*
+ * One IPv6 extension chain (Some(ExtensionHeaders), headers.rs:19-28), 16 B:
+ * len = IPv6Reader::extension_headers_len (ipv6.rs:141), off[k] = start of
+ * slot k relative to the IPv6 payload (frame offset ip + 40 + off[k]).
+ *
+ * The ext side array of a batch of n frames holds 2n entries:
+ *   ext[i]     the outer ipv6 chain of frame i, valid iff flags & ZP_F_EXT;
+ *   ext[n + i] the ip_in_ip IPv6 chain,           valid iff flags & ZP_F_INNER_EXT.
+ * Entries whose flag is clear are unspecified (the kernel may leave them
+ * untouched or zero them). Passing ext = NULL drops the chains (the records
+ * still carry their presence bits, ext lengths excepted).
+ */
 typedef struct zp_ext_offsets {
+    uint16_t len;
     uint16_t off[ZP_EXT_SLOTS];
+    uint16_t reserved;
 } zp_ext_offsets;
 
 /* ------------------------------------------------------------------------- */
@@ -159,7 +170,8 @@ const char* zp_last_error(void);
  * HIP device; the call only enqueues work on `stream` (a hipStream_t, NULL =
  * default stream) and returns. Frames may lie anywhere in `arena` (gaps,
  * overlaps and any order are allowed); the fast path is taken for the common
- * packed, increasing layout. `inner_ext` may be NULL. Returns 0 on success or
+ * packed, increasing layout. `ext` (2n entries, see zp_ext_offsets) may be
+ * NULL. Returns 0 on success or
  * a negative value if the launch failed (see zp_last_error()).
  * Precondition (not checked on the device: the descriptors live in HBM and the
  * call does not synchronise): offs[i] + lens[i] <= the arena's size for every
@@ -169,7 +181,7 @@ const char* zp_last_error(void);
  */
 int zp_parse_batch_device(const uint8_t* arena, const uint64_t* offs,
                           const uint32_t* lens, uint64_t n,
-                          zp_record* records, zp_ext_offsets* inner_ext,
+                          zp_record* records, zp_ext_offsets* ext,
                           void* stream);
 
 /* Host-buffer convenience path: the frames, descriptors and outputs live in
@@ -184,7 +196,7 @@ zp_ctx* zp_ctx_create(int device, uint64_t chunk_bytes);
 void    zp_ctx_destroy(zp_ctx* ctx);
 int zp_parse_batch_host(zp_ctx* ctx, const uint8_t* arena, uint64_t arena_bytes,
                         const uint64_t* offs, const uint32_t* lens, uint64_t n,
-                        zp_record* records, zp_ext_offsets* inner_ext);
+                        zp_record* records, zp_ext_offsets* ext);
 /* The same over several devices (one context each, e.g. the 8 GPUs of a
  * node): contiguous frame ranges with balanced byte totals run concurrently,
  * one host thread per context. No cross-device exchange. Returns 0 or the
@@ -192,11 +204,12 @@ int zp_parse_batch_host(zp_ctx* ctx, const uint8_t* arena, uint64_t arena_bytes,
 int zp_parse_batch_host_multi(zp_ctx* const* ctxs, int nctx, const uint8_t* arena,
                               uint64_t arena_bytes, const uint64_t* offs,
                               const uint32_t* lens, uint64_t n, zp_record* records,
-                              zp_ext_offsets* inner_ext);
-/* One frame through the GPU path (PacketParser::parse equivalent).
- * Returns the zp_err code (>= 0) or a negative value on HIP failure. */
+                              zp_ext_offsets* ext);
+/* One frame through the GPU path (PacketParser::parse equivalent). ext: NULL
+ * or 2 entries (outer, ip_in_ip chain). Returns the zp_err code (>= 0) or a
+ * negative value on HIP failure. */
 int zp_parse_one(zp_ctx* ctx, const uint8_t* frame, uint64_t len,
-                 zp_record* record, zp_ext_offsets* inner_ext);
+                 zp_record* record, zp_ext_offsets ext[2]);
 
 /* ------------------------------------------------------------------------- */
 /* Host-ring ingestion pipeline. Frames start in host */
@@ -221,7 +234,7 @@ typedef struct zp_ring_slot {
     uint32_t* lens;                     /* pinned frame lengths                */
     uint64_t arena_cap, frames_cap;
     const zp_record* records;           /* results (valid after wait/poll)     */
-    const zp_ext_offsets* inner_ext;    /* written where ZP_F_INNER_EXT is set */
+    const zp_ext_offsets* ext;          /* 2n entries (zp_ext_offsets), n below */
     uint64_t n;                         /* frames in the slot (after wait/poll) */
     uint64_t seq;                       /* submission sequence number          */
 } zp_ring_slot;
@@ -303,7 +316,7 @@ int zp_extract_columns_device(const uint8_t* arena, const uint64_t* offs,
  * Same results as the two calls in sequence. */
 int zp_parse_batch_columns_device(const uint8_t* arena, const uint64_t* offs,
                                   const uint32_t* lens, uint64_t n, zp_record* records,
-                                  zp_ext_offsets* inner_ext, void* const* cols, void* stream);
+                                  zp_ext_offsets* ext, void* const* cols, void* stream);
 
 /* ------------------------------------------------------------------------- */
 /* Batched PacketBuilder. The reference builds one    */

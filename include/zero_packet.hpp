@@ -319,10 +319,15 @@ struct PacketParser {
     std::optional<Icmpv6Reader> icmpv6;
 
     // Rebuilds the parse result of `frame` from its record (no re-parse).
+    // outer / inner: the frame's zp_ext_offsets entries (ext[i], ext[n + i]
+    // of the batch), needed when the record flags that chain.
     // Throws zp::Error when the record holds an error (the reference's Err).
     static PacketParser from_record(Bytes frame, const zp_record& r,
+                                    const zp_ext_offsets* outer = nullptr,
                                     const zp_ext_offsets* inner = nullptr) {
         if (r.err) detail::fail(r.err);
+        if (((r.flags & ZP_F_EXT) && !outer) || ((r.flags & ZP_F_INNER_EXT) && !inner))
+            throw std::invalid_argument("from_record: the record flags an extension chain");
         PacketParser p;
         const size_t hl = r.eth_len;
         if (r.flags & ZP_F_ETHERNET) p.ethernet.emplace(frame, hl);
@@ -331,9 +336,9 @@ struct PacketParser {
         if (r.flags & ZP_F_IPV6) {
             IPv6Reader v6(frame.sub(hl));
             if (r.flags & ZP_F_EXT) {
-                v6.extension_headers = ext(frame, hl + 40, r.flags, 12, r.ext_off, r.ext_len,
+                v6.extension_headers = ext(frame, hl + 40, r.flags, 12, outer->off, outer->len,
                                            r.final_nh);
-                v6.extension_headers_len = r.ext_len;
+                v6.extension_headers_len = outer->len;
             }
             p.ipv6 = v6;
         }
@@ -343,11 +348,9 @@ struct PacketParser {
                 ii.kind = IpInIp::Kind::Ipv6;
                 IPv6Reader v6(frame.sub(r.inner_off));
                 if (r.flags & ZP_F_INNER_EXT) {
-                    static const uint16_t zero[ZP_EXT_SLOTS] = {0, 0, 0, 0, 0, 0};
-                    v6.extension_headers = ext(frame, r.inner_off + 40, r.flags, 18,
-                                               inner ? inner->off : zero, r.inner_ext_len,
-                                               r.inner_final_nh);
-                    v6.extension_headers_len = r.inner_ext_len;
+                    v6.extension_headers = ext(frame, r.inner_off + 40, r.flags, 18, inner->off,
+                                               inner->len, r.inner_final_nh);
+                    v6.extension_headers_len = inner->len;
                 }
                 ii.ipv6 = v6;
             } else {
@@ -367,13 +370,14 @@ struct PacketParser {
     // PacketParser::parse (parser.rs:53) for one frame, through the GPU path
     // (zp_parse_one on `ctx`). Throws zp::Error on a parse error and
     // std::runtime_error on a HIP failure.
-    static PacketParser parse(zp_ctx* ctx, Bytes frame, zp_ext_offsets* inner_out = nullptr) {
+    // ext_out (optional, 2 entries) receives the outer and ip_in_ip chains.
+    static PacketParser parse(zp_ctx* ctx, Bytes frame, zp_ext_offsets* ext_out = nullptr) {
         zp_record r{};
-        zp_ext_offsets e{};
-        const int rc = zp_parse_one(ctx, frame.ptr, frame.len, &r, &e);
+        zp_ext_offsets e[2] = {};
+        const int rc = zp_parse_one(ctx, frame.ptr, frame.len, &r, e);
         if (rc < 0) throw std::runtime_error(std::string("zp_parse_one: ") + zp_last_error());
-        if (inner_out) *inner_out = e;
-        return from_record(frame, r, &e);
+        if (ext_out) { ext_out[0] = e[0]; ext_out[1] = e[1]; }
+        return from_record(frame, r, &e[0], &e[1]);
     }
 
 private:
@@ -405,15 +409,16 @@ public:
     Context& operator=(const Context&) = delete;
     zp_ctx* get() const { return ctx_; }
 
-    // n frames of a host buffer -> host records (H2D, parse, D2H).
+    // n frames of a host buffer -> host records (H2D, parse, D2H); ext:
+    // nullptr or 2n entries (zero_packet.h, zp_ext_offsets).
     void parse_batch(const uint8_t* arena, uint64_t arena_bytes, const uint64_t* offs,
                      const uint32_t* lens, uint64_t n, zp_record* records,
-                     zp_ext_offsets* inner_ext = nullptr) {
-        if (zp_parse_batch_host(ctx_, arena, arena_bytes, offs, lens, n, records, inner_ext) < 0)
+                     zp_ext_offsets* ext = nullptr) {
+        if (zp_parse_batch_host(ctx_, arena, arena_bytes, offs, lens, n, records, ext) < 0)
             throw std::runtime_error(std::string("zp_parse_batch_host: ") + zp_last_error());
     }
-    PacketParser parse(Bytes frame, zp_ext_offsets* inner_out = nullptr) {
-        return PacketParser::parse(ctx_, frame, inner_out);
+    PacketParser parse(Bytes frame, zp_ext_offsets* ext_out = nullptr) {
+        return PacketParser::parse(ctx_, frame, ext_out);
     }
 private:
     zp_ctx* ctx_;
@@ -423,20 +428,20 @@ private:
 // contiguous ranges, concurrently (zp_parse_batch_host_multi).
 inline void parse_batch_multi(Context* const* ctxs, int nctx, const uint8_t* arena,
                               uint64_t arena_bytes, const uint64_t* offs, const uint32_t* lens,
-                              uint64_t n, zp_record* records, zp_ext_offsets* inner_ext = nullptr) {
+                              uint64_t n, zp_record* records, zp_ext_offsets* ext = nullptr) {
     zp_ctx* raw[64];
     if (nctx < 1 || nctx > 64) throw std::invalid_argument("parse_batch_multi: 1..64 contexts");
     for (int d = 0; d < nctx; ++d) raw[d] = ctxs[d]->get();
     if (zp_parse_batch_host_multi(raw, nctx, arena, arena_bytes, offs, lens, n, records,
-                                  inner_ext) < 0)
+                                  ext) < 0)
         throw std::runtime_error(std::string("zp_parse_batch_host_multi: ") + zp_last_error());
 }
 
 // Device-resident batch (the hot path): enqueue on a hipStream_t (void*).
 inline void parse_batch_device(const uint8_t* arena, const uint64_t* offs, const uint32_t* lens,
-                               uint64_t n, zp_record* records, zp_ext_offsets* inner_ext,
+                               uint64_t n, zp_record* records, zp_ext_offsets* ext,
                                void* stream) {
-    if (zp_parse_batch_device(arena, offs, lens, n, records, inner_ext, stream) < 0)
+    if (zp_parse_batch_device(arena, offs, lens, n, records, ext, stream) < 0)
         throw std::runtime_error(std::string("zp_parse_batch_device: ") + zp_last_error());
 }
 

@@ -352,21 +352,31 @@ static int parse(parser_t* ps, slice_t bytes) {
 
 /* ---- record encoding (include/zero_packet.h) ----------------------------- */
 
-static void ext_to_record(const ipv6_t* r, uint32_t shift, uint32_t* flags, uint16_t off[6]) {
+/* One Option<ExtensionHeaders> (headers.rs:19-28) -> slot bits + a
+ * zp_ext_offsets entry (len = extension_headers_len, ipv6.rs:141). */
+static void ext_to_record(const ipv6_t* r, uint32_t shift, uint32_t* flags, zp_ext_offsets* x) {
+    x->len = (uint16_t)r->extension_headers_len;
     for (int k = 0; k < ZP_EXT_SLOTS; ++k) {
         if (r->ext.h[k].present) {
             *flags |= 1u << (shift + k);
-            off[k] = (uint16_t)r->ext.h[k].start;
+            x->off[k] = (uint16_t)r->ext.h[k].start;
         }
     }
 }
 
-int zpo_parse(const uint8_t* frame, size_t len, zp_record* rec, zp_ext_offsets* inner) {
+/* One frame: the record, and (xo / xi non-NULL) the outer and ip_in_ip
+ * extension chains; entries without a chain are zero. */
+int zpo_parse(const uint8_t* frame, size_t len, zp_record* rec, zp_ext_offsets* xo,
+              zp_ext_offsets* xi) {
     parser_t ps;
     slice_t s = {frame, len};
     int err = parse(&ps, s);
+    zp_ext_offsets to, ti;
     memset(rec, 0, sizeof *rec);
-    if (inner) memset(inner, 0, sizeof *inner);
+    memset(&to, 0, sizeof to);
+    memset(&ti, 0, sizeof ti);
+    if (xo) *xo = to;
+    if (xi) *xi = ti;
     if (err) { rec->err = (uint8_t)err; return err; }
     uint32_t f = 0;
     if (ps.ethernet.present) f |= ZP_F_ETHERNET;
@@ -382,8 +392,8 @@ int zpo_parse(const uint8_t* frame, size_t len, zp_record* rec, zp_ext_offsets* 
         rec->final_nh = ipv6_final_nh(&ps.outer6);
         if (ps.outer6.has_ext) {
             f |= ZP_F_EXT;
-            rec->ext_len = (uint16_t)ps.outer6.extension_headers_len;
-            ext_to_record(&ps.outer6, 12, &f, rec->ext_off);
+            ext_to_record(&ps.outer6, 12, &f, &to);
+            if (xo) *xo = to;
         }
     }
     if (ps.ip_in_ip.present) {
@@ -393,12 +403,9 @@ int zpo_parse(const uint8_t* frame, size_t len, zp_record* rec, zp_ext_offsets* 
             f |= ZP_F_IP_IN_IP_V6;
             rec->inner_final_nh = ipv6_final_nh(&ps.inner6);
             if (ps.inner6.has_ext) {
-                zp_ext_offsets tmp;
-                memset(&tmp, 0, sizeof tmp);
                 f |= ZP_F_INNER_EXT;
-                rec->inner_ext_len = (uint16_t)ps.inner6.extension_headers_len;
-                ext_to_record(&ps.inner6, 18, &f, tmp.off);
-                if (inner) *inner = tmp;
+                ext_to_record(&ps.inner6, 18, &f, &ti);
+                if (xi) *xi = ti;
             }
         }
     }
@@ -413,21 +420,23 @@ typedef struct {
     const uint64_t* offs;
     const uint32_t* lens;
     zp_record* recs;
-    zp_ext_offsets* inner;
-    uint64_t lo, hi;
+    zp_ext_offsets* ext;        /* 2n entries or NULL */
+    uint64_t n, lo, hi;
 } job_t;
 
 static void* worker(void* a) {
     job_t* j = (job_t*)a;
     for (uint64_t i = j->lo; i < j->hi; ++i)
-        zpo_parse(j->arena + j->offs[i], j->lens[i], &j->recs[i], j->inner ? &j->inner[i] : 0);
+        zpo_parse(j->arena + j->offs[i], j->lens[i], &j->recs[i], j->ext ? &j->ext[i] : 0,
+                  j->ext ? &j->ext[j->n + i] : 0);
     return 0;
 }
 
 /* Parses n frames with `nthreads` threads over contiguous shards
- * (nthreads <= 0: all online cores). Returns the thread count used. */
+ * (nthreads <= 0: all online cores); ext: NULL or 2n entries laid out as
+ * zp_parse_batch_device's. Returns the thread count used. */
 int zpo_parse_batch(const uint8_t* arena, const uint64_t* offs, const uint32_t* lens,
-                    uint64_t n, zp_record* recs, zp_ext_offsets* inner, int nthreads) {
+                    uint64_t n, zp_record* recs, zp_ext_offsets* ext, int nthreads) {
     if (nthreads <= 0) nthreads = (int)sysconf(_SC_NPROCESSORS_ONLN);
     if (nthreads > 256) nthreads = 256;
     if (nthreads < 1) nthreads = 1;
@@ -435,7 +444,7 @@ int zpo_parse_batch(const uint8_t* arena, const uint64_t* offs, const uint32_t* 
     int started[256];
     job_t jobs[256];
     for (int t = 0; t < nthreads; ++t) {
-        jobs[t] = (job_t){arena, offs, lens, recs, inner, n * t / nthreads, n * (t + 1) / nthreads};
+        jobs[t] = (job_t){arena, offs, lens, recs, ext, n, n * t / nthreads, n * (t + 1) / nthreads};
         started[t] = 0;
         if (nthreads == 1) { worker(&jobs[t]); continue; }
         if (pthread_create(&th[t], 0, worker, &jobs[t]) == 0) started[t] = 1;

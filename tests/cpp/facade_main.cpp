@@ -1,5 +1,5 @@
 // Test driver for include/zero_packet.hpp (the C++ facade).
-//   facade_main cpu   stdin lines "<frame hex> <zp_record hex> <zp_ext_offsets hex>"
+//   facade_main cpu   stdin lines "<frame hex> <zp_record hex> <2 x zp_ext_offsets hex>"
 //                     -> PacketParser::from_record (no GPU, no library)
 //   facade_main gpu   stdin lines "<frame hex>" -> PacketParser::parse through
 //                     zp_parse_one (libzp_hip.so, the GPU path)
@@ -94,11 +94,11 @@ int main(int argc, char** argv) {
 #endif
             } else {
                 zp_record r{};
-                zp_ext_offsets e{};
+                zp_ext_offsets e[2] = {};
                 const auto rv = unhex(rh), ev = unhex(eh);
                 std::memcpy(&r, rv.data(), sizeof r);
-                std::memcpy(&e, ev.data(), sizeof e);
-                p = zp::PacketParser::from_record(b, r, &e);
+                std::memcpy(e, ev.data(), sizeof e);       // outer, ip_in_ip chain
+                p = zp::PacketParser::from_record(b, r, &e[0], &e[1]);
             }
             std::cout << summary(p) << "\n";
         } catch (const zp::Error& e) {

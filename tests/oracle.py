@@ -16,9 +16,8 @@ _lib = None
 RECORD_DTYPE = np.dtype([
     ("flags", "<u4"), ("err", "u1"), ("eth_len", "u1"), ("final_nh", "u1"),
     ("inner_final_nh", "u1"), ("inner_off", "<u4"), ("l4_off", "<u4"),
-    ("ext_len", "<u2"), ("ext_off", "<u2", (6,)), ("inner_ext_len", "<u2"),
 ])
-EXT_DTYPE = np.dtype([("off", "<u2", (6,))])
+EXT_DTYPE = np.dtype([("len", "<u2"), ("off", "<u2", (6,)), ("reserved", "<u2")])
 
 
 def lib():
@@ -29,7 +28,7 @@ def lib():
         l = ctypes.CDLL(LIB)
         vp, u64, i32, sz = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_size_t
         l.zpo_parse.restype = i32
-        l.zpo_parse.argtypes = [vp, sz, vp, vp]
+        l.zpo_parse.argtypes = [vp, sz, vp, vp, vp]
         l.zpo_parse_batch.restype = i32
         l.zpo_parse_batch.argtypes = [vp, vp, vp, u64, vp, vp, i32]
         l.zpo_internet_checksum.restype = ctypes.c_uint16
@@ -41,13 +40,24 @@ def lib():
 
 
 def parse_one(frame):
-    """-> (err, record[RECORD_DTYPE], inner_ext[EXT_DTYPE])"""
+    """-> (err, record[RECORD_DTYPE], ext[EXT_DTYPE] (2,): outer, ip_in_ip chain)"""
     frame = bytes(frame)
     buf = ctypes.create_string_buffer(frame, max(len(frame), 1))
     rec = np.zeros(1, RECORD_DTYPE)
-    ext = np.zeros(1, EXT_DTYPE)
-    err = lib().zpo_parse(ctypes.addressof(buf), len(frame), rec.ctypes.data, ext.ctypes.data)
-    return err, rec[0], ext[0]
+    ext = np.zeros(2, EXT_DTYPE)
+    err = lib().zpo_parse(ctypes.addressof(buf), len(frame), rec.ctypes.data, ext[0:].ctypes.data,
+                          ext[1:].ctypes.data)
+    return err, rec[0], ext
+
+
+def record_tuple(rec, ext):
+    """(err, flags, eth_len, final_nh, inner_final_nh, inner_off, l4_off,
+    ext_len, ext_off tuple, inner_ext_len, inner ext_off tuple) of one frame
+    (ext: its two zp_ext_offsets entries; zero where there is no chain)."""
+    return (int(rec["err"]), int(rec["flags"]), int(rec["eth_len"]), int(rec["final_nh"]),
+            int(rec["inner_final_nh"]), int(rec["inner_off"]), int(rec["l4_off"]),
+            int(ext[0]["len"]), tuple(int(x) for x in ext[0]["off"]),
+            int(ext[1]["len"]), tuple(int(x) for x in ext[1]["off"]))
 
 
 def parse_batch(arena, offs, lens, nthreads=0):
@@ -56,7 +66,7 @@ def parse_batch(arena, offs, lens, nthreads=0):
     lens = np.ascontiguousarray(lens).astype(np.uint32, copy=False)
     n = len(offs)
     rec = np.zeros(n, RECORD_DTYPE)
-    ext = np.zeros(n, EXT_DTYPE)
+    ext = np.zeros((2, n), EXT_DTYPE)
     if n:
         lib().zpo_parse_batch(arena.ctypes.data, offs.ctypes.data, lens.ctypes.data, n,
                               rec.ctypes.data, ext.ctypes.data, nthreads)

@@ -50,7 +50,7 @@ def test_err_strings(zp):
         35: "IPv6 encapsulated checksum is invalid.",
     }
     lib = zp._lib.hip()
-    assert lib.zp_abi_version() == 1
+    assert lib.zp_abi_version() == 2
     assert lib.zp_err_str(0) == b""
     for code, s in want.items():
         assert lib.zp_err_str(code).decode() == s
@@ -60,11 +60,13 @@ def test_err_strings(zp):
 
 
 def test_record_layout(zp):
-    assert zp.records.RECORD_DTYPE.itemsize == 32
-    assert zp.records.RECORD_DTYPE.fields["inner_off"][1] == 8
-    assert zp.records.RECORD_DTYPE.fields["l4_off"][1] == 12
-    assert zp.records.RECORD_DTYPE.fields["ext_off"][1] == 18
-    assert zp.records.RECORD_DTYPE.fields["inner_ext_len"][1] == 30
+    """zp_record / zp_ext_offsets (ABI v2) as the numpy dtypes see them."""
+    r, e = zp.records.RECORD_DTYPE, zp.records.EXT_DTYPE
+    assert r.itemsize == 16 and e.itemsize == 16
+    assert r.fields["err"][1] == 4 and r.fields["eth_len"][1] == 5
+    assert r.fields["inner_off"][1] == 8
+    assert r.fields["l4_off"][1] == 12
+    assert e.fields["len"][1] == 0 and e.fields["off"][1] == 2
 
 
 def test_no_cpu_fallback(zp):

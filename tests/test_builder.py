@@ -96,10 +96,10 @@ def test_oracle_builder_very_complex_packet(zp):
             .ipv4(4, 5, 0, 0, 150, 0, 0, 0, 64, 6, IP1, IP2)
             .tcp(IP1, 99, IP2, 11, 123, 321, 11, 99, 99, 4321, 1234, pay).build())
     assert f == want
-    err, rec, _ = orc.parse_one(f)
+    err, rec, ext = orc.parse_one(f)
     assert err == 0 and rec["eth_len"] == 22 and rec["inner_off"] == 150 and rec["l4_off"] == 170
     # slot order hop_by_hop, routing, fragment, auth, dest1, dest2 (headers.rs:20-25)
-    assert list(rec["ext_off"]) == [0, 32, 48, 56, 16, 72]
+    assert list(ext[0]["off"]) == [0, 32, 48, 56, 16, 72]
     assert res[0]["header_len"] == 170 + 44
 
 

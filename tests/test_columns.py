@@ -132,7 +132,7 @@ def test_oracle_columns_vs_getters(zp, golden):
     cols = orc.columns(arena, offs, lens, recs)
     nok = 0
     for i, f in enumerate(frames):
-        want = getter_columns(zp, f, recs[i], ext[i])
+        want = getter_columns(zp, f, recs[i], ext[:, i])
         nok += int(recs[i]["err"]) == 0
         for name, _, _ in orc.COLUMN_SPEC:
             assert np.array_equal(cols[name][i], want[name]), (i, name, f.hex())

@@ -41,7 +41,7 @@ def _worker(rank, world, port, q):
         rec, ext = orc.parse_batch(sub, o, ln, 1)
         mine = torch.from_numpy(np.frombuffer(rec.tobytes() + ext.tobytes(), np.uint8).copy())
         parts = [None] * world
-        dist.all_gather_object(parts, (lo, hi, rec.tobytes(), ext.tobytes()))
+        dist.all_gather_object(parts, (lo, hi, rec.tobytes(), ext[0].tobytes(), ext[1].tobytes()))
         # bench.py's reduction: the slowest rank defines the step time
         t = torch.tensor([float(rank + 1)], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -108,7 +108,8 @@ def test_world2_gloo_shards_match_single_process():
     assert parts[0][0] == 0 and parts[-1][1] == 3000
     assert all(parts[r][1] == parts[r + 1][0] for r in range(world - 1))
     assert b"".join(p[2] for p in parts) == rec.tobytes()
-    assert b"".join(p[3] for p in parts) == ext.tobytes()
+    assert b"".join(p[3] for p in parts) == ext[0].tobytes()    # outer chains
+    assert b"".join(p[4] for p in parts) == ext[1].tobytes()    # ip_in_ip chains
     assert (rec["err"] != 0).sum() >= 2
     # per-rank weak-scaling shards are consecutive slices of one packet stream
     a, o, l = zp.batch.generate_host("c3", 400)

@@ -49,14 +49,15 @@ def gpu_parse(zp, arena, offs, lens, base_shift=0):
 
 
 def assert_same(got, got_ext, want, want_ext):
-    bad = np.nonzero(got.view(np.uint8).reshape(-1, 32).any(1) !=
-                     want.view(np.uint8).reshape(-1, 32).any(1))[0]
-    diff = np.nonzero((got.view(np.uint8).reshape(-1, 32) !=
-                       want.view(np.uint8).reshape(-1, 32)).any(1))[0]
+    """Records byte-identical; the extension chains the records flag
+    identical (records.ext_match; other ext entries are unspecified)."""
+    g = got.view(np.uint8).reshape(-1, 16)
+    w = want.view(np.uint8).reshape(-1, 16)
+    diff = np.nonzero((g != w).any(1))[0]
     assert len(diff) == 0, (f"{len(diff)} records differ; first {diff[:5]}",
-                            got[diff[:3]], want[diff[:3]], bad[:3])
-    m = (want["flags"] & (1 << 11)) != 0
-    assert got_ext[m].tobytes() == want_ext[m].tobytes()
+                            got[diff[:3]], want[diff[:3]])
+    from importlib import import_module
+    assert import_module("zero-packet_amd").records.ext_match(got_ext, want_ext, want)
 
 
 # ---- golden packets ------------------------------------------------------
@@ -68,7 +69,7 @@ def test_golden_batch(zp, golden):
         got, gext = gpu_parse(zp, arena, offs, lens, base_shift=shift)
         want, wext = orc.parse_batch(arena, offs, lens)
         assert_same(got, gext, want, wext)
-        for fx, f, r, e in zip(golden["fixtures"], frames, got, gext):
+        for fx, f, r, e in zip(golden["fixtures"], frames, got, gext.T):
             check_expect(zp, f, r, e, fx["expect"])
 
 
@@ -240,7 +241,7 @@ def test_host_path(zp, golden, pinned):
     ctx = lib.zp_ctx_create(0, 1 << 20)           # small chunks: many slots in flight
     assert ctx
     rec = np.zeros(len(offs), zp.records.RECORD_DTYPE)
-    ext = np.zeros(len(offs), zp.records.EXT_DTYPE)
+    ext = np.zeros((2, len(offs)), zp.records.EXT_DTYPE)
     rc = lib.zp_parse_batch_host(ctx, arena.ctypes.data, len(arena), offs.ctypes.data,
                                  lens.ctypes.data, len(offs), rec.ctypes.data, ext.ctypes.data)
     lib.zp_ctx_destroy(ctx)
@@ -259,7 +260,7 @@ def test_host_path_multi(zp, golden):
     assert all(ctxs)
     arr = (ctypes.c_void_p * 3)(*ctxs)
     rec = np.zeros(len(offs), zp.records.RECORD_DTYPE)
-    ext = np.zeros(len(offs), zp.records.EXT_DTYPE)
+    ext = np.zeros((2, len(offs)), zp.records.EXT_DTYPE)
     rc = lib.zp_parse_batch_host_multi(arr, 3, arena.ctypes.data, len(arena), offs.ctypes.data,
                                        lens.ctypes.data, len(offs), rec.ctypes.data,
                                        ext.ctypes.data)
@@ -282,9 +283,10 @@ def test_full_size_properties(zp, config, n):
     from importlib import import_module
     rec = import_module("zero-packet_amd.records")
     arena, offs, lens = zp.batch.generate(config, n, device=dev())
-    r1, e1 = zp.batch.parse_batch(arena, offs, lens)
+    zeros = lambda: torch.zeros((2, n, 16), dtype=torch.uint8, device=arena.device)
+    r1, e1 = zp.batch.parse_batch(arena, offs, lens, ext=zeros())
     assert int((r1[:, 4] != 0).sum()) == 0
-    r2, e2 = zp.batch.parse_batch(arena, offs, lens)
+    r2, e2 = zp.batch.parse_batch(arena, offs, lens, ext=zeros())
     assert torch.equal(r1, r2) and torch.equal(e1, e2)
     idx = torch.randint(0, n, (2000,), device=arena.device, generator=torch.Generator(
         device=arena.device).manual_seed(1))
@@ -292,7 +294,7 @@ def test_full_size_properties(zp, config, n):
     frames = [arena[int(o):int(o) + int(l)].cpu().numpy() for o, l in zip(so, sl)]
     sa, sof, sle = pack([f.tobytes() for f in frames])
     want, wext = orc.parse_batch(sa, sof, sle)
-    got, gext = zp.batch.records_to_numpy(r1[idx], e1[idx])
+    got, gext = zp.batch.records_to_numpy(r1[idx], e1[:, idx])
     assert_same(got, gext, want, wext)
     flags = r1[:, 0:4].contiguous().view(torch.int32)[:, 0]
     ipip = (flags & rec.F_IP_IN_IP) != 0
@@ -329,7 +331,7 @@ def test_max_size_full_imix_one_gpu(zp):
     del arena
     sa, sof, sle = pack(frames)
     want, wext = orc.parse_batch(sa, sof, sle)
-    got, gext = zp.batch.records_to_numpy(rec[idx], ext[idx])
+    got, gext = zp.batch.records_to_numpy(rec[idx], ext[:, idx])
     assert_same(got, gext, want, wext)
 
 
@@ -349,9 +351,9 @@ def test_descriptor_bounds_refused(zp):
     with pytest.raises(ValueError):
         zp.batch.parse_batch(a, torch.tensor([0, -64], dtype=torch.int64, device=d), good)
     with pytest.raises(ValueError):
-        zp.batch.parse_batch(a, o, good, records=torch.empty((2, 16), dtype=torch.uint8, device=d))
+        zp.batch.parse_batch(a, o, good, records=torch.empty((2, 8), dtype=torch.uint8, device=d))
     with pytest.raises(ValueError):
-        zp.batch.parse_batch(a, o, good, inner_ext=torch.empty((2, 12), dtype=torch.uint8))
+        zp.batch.parse_batch(a, o, good, ext=torch.empty((2, 2, 16), dtype=torch.uint8))
     with pytest.raises(ValueError):
         zp.columns.parse_with_columns(a, o, torch.tensor([64, 600], dtype=torch.int32, device=d))
     r, _ = zp.batch.parse_batch(a, o, good)

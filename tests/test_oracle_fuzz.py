@@ -11,10 +11,7 @@ from test_oracle_golden import ERR
 
 
 def rec_tuple(rec, ext):
-    return (int(rec["err"]), int(rec["flags"]), int(rec["eth_len"]), int(rec["final_nh"]),
-            int(rec["inner_final_nh"]), int(rec["inner_off"]), int(rec["l4_off"]),
-            int(rec["ext_len"]), tuple(int(x) for x in rec["ext_off"]),
-            int(rec["inner_ext_len"]), tuple(int(x) for x in ext["off"]))
+    return orc.record_tuple(rec, ext)
 
 
 def mutate(rng, frame):

@@ -30,8 +30,7 @@ def test_ring_parse_matches_oracle(zp, cfg, slots, slot_bytes):
     with zp.ring.Ring(0, slots, slot_bytes) as ring:
         got, gext = ring.parse(arena, offs, lens)
     assert got.tobytes() == want.tobytes()
-    m = (want["flags"] & zp.records.F_INNER_EXT) != 0
-    assert gext[m].tobytes() == wext[m].tobytes()
+    assert zp.records.ext_match(gext, wext, want)
 
 
 @pytest.mark.gpu

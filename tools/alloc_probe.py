@@ -45,12 +45,14 @@ def main():
     ap.add_argument("--variants", default="", help="comma list of tools/variants/libzp_<name>.so")
     ap.add_argument("--no-check", action="store_true", help="time variants whose records differ (ablations)")
     ap.add_argument("--parse-only", action="store_true", help="no membw kernels (PMC runs)")
+    ap.add_argument("--move-records", action="store_true",
+                    help="keep the arena, move the records buffer (and variants) instead")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     arena, offs, lens = zp.batch.generate(a.config, a.packets, device=dev)
     n = a.packets
-    records = torch.empty((n, 32), dtype=torch.uint8, device=dev)
-    inner = torch.zeros((n, 12), dtype=torch.uint8, device=dev)
+    records = torch.empty((n, 16), dtype=torch.uint8, device=dev)
+    inner = torch.empty((2, n, 16), dtype=torch.uint8, device=dev)
     nb = arena.numel()
     mb = ctypes.CDLL(os.path.join(ROOT, "tools", "libmembw.so"))
     mb.membw_read.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
@@ -105,6 +107,21 @@ def main():
                                                        rout.data_ptr(), reg, 0, None))
         print(json.dumps({name: r}), flush=True)
 
+    if a.move_records:
+        hold = []
+        for k in range(a.copies):
+            hold.append(torch.empty(97 << 20, dtype=torch.uint8, device=dev))   # shift the next block
+            rec2 = torch.empty((n, 16), dtype=torch.uint8, device=dev)
+            r = timeit(arena, offs, lens, rec2, inner, a.steps)
+            r["rec_ptr"] = hex(rec2.data_ptr())
+            s = torch.cuda.current_stream()
+            for vname, vl in variants.items():
+                r[vname] = bw(lambda: vl.zp_parse_batch_device(
+                    arena.data_ptr(), offs.data_ptr(), lens.data_ptr(), n, rec2.data_ptr(),
+                    inner.data_ptr(), ctypes.c_void_p(s.cuda_stream)))
+            print(json.dumps({f"records{k}": r}), flush=True)
+            hold.append(rec2)
+        return
     probe("base", arena)
     live = []
     for k in range(a.copies):

@@ -34,8 +34,8 @@ def main():
     for cfg in a.configs.split(","):
         n = {"c3": 1 << 24, "c4": 1 << 24, "c5": 1 << 25, "c2": 1 << 20}[cfg]
         arena, offs, lens = zp.batch.generate(cfg, n, device=d)
-        rec = torch.empty((n, 32), dtype=torch.uint8, device=d)
-        ext = torch.zeros((n, 12), dtype=torch.uint8, device=d)
+        rec = torch.empty((n, 16), dtype=torch.uint8, device=d)
+        ext = torch.empty((2, n, 16), dtype=torch.uint8, device=d)
         cols = [torch.empty(n * zp.columns.width(c), dtype=torch.uint8, device=d)
                 for c in zp.columns.NAMES]
         ptrs = (ctypes.c_void_p * len(cols))(*[c.data_ptr() for c in cols])

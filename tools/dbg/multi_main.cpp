@@ -14,7 +14,7 @@ int main() {
     for (uint64_t i = 0; i < n; ++i) { lens[i] = 64 + (i * 37) % 1400; offs[i] = pos; pos += lens[i]; }
     std::vector<uint8_t> arena(pos + 64, 0x5a);
     std::vector<zp_record> rec(n);
-    std::vector<zp_ext_offsets> ext(n);
+    std::vector<zp_ext_offsets> ext(2 * n);   // outer chains, then ip_in_ip chains
     zp_ctx* ctx[3];
     for (int d = 0; d < 3; ++d) { ctx[d] = zp_ctx_create(0, 1 << 20); if (!ctx[d]) { printf("ctx fail %s\n", zp_last_error()); return 1; } }
     int rc = zp_parse_batch_host(ctx[0], arena.data(), arena.size(), offs.data(), lens.data(), n, rec.data(), ext.data());

@@ -101,7 +101,7 @@ def main():
     if args.c2cold:
         n = 1 << 20
         copies = [zp.batch.generate("c2", n, device=dev) for _ in range(8)]
-        rec = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+        rec = torch.empty((n, 16), dtype=torch.uint8, device=dev)
         lib = zp._lib.hip()
         nbytes = int(copies[0][2].to(torch.int64).sum())
         for label, order in (("warm (same copy)", [0] * 8), ("cold (8 rotating copies)",
@@ -127,8 +127,8 @@ def main():
     for cfg in [c for c in args.configs.split(",") if c]:
         n = sizes[cfg]
         arena, offs, lens = zp.batch.generate(cfg, n, device=dev)
-        rec = torch.empty((n, 32), dtype=torch.uint8, device=dev)
-        ext = torch.zeros((n, 12), dtype=torch.uint8, device=dev)
+        rec = torch.empty((n, 16), dtype=torch.uint8, device=dev)
+        ext = torch.empty((2, n, 16), dtype=torch.uint8, device=dev)
         nbytes = int(lens.to(torch.int64).sum())
         ref = None
         res = {k: [] for k in libs}
@@ -163,7 +163,7 @@ def main():
                       f"  (write+read {(wbytes + rbytes) / med / 1e6:6.0f} GB/s)  "
                       f"{n / med / 1e3:8.0f} Mpkt/s", flush=True)
                 ms = time_launches(lambda: zp.columns.parse_with_columns(
-                    arena, offs, lens, names=names, records=rec, inner_ext=ext, out=out, check=False),
+                    arena, offs, lens, names=names, records=rec, ext=ext, out=out, check=False),
                     args.reps * args.rounds)
                 med = float(np.median(ms))
                 print(f"{cfg} fused parse+columns[{label}]: {med:8.3f} ms  "

@@ -27,8 +27,8 @@ def main():
     torch.cuda.synchronize()
     nbytes = int(lens.to(torch.int64).sum().item())
     print(f"generated {n} frames, {nbytes / 1e9:.1f} GB in {time.time() - t0:.1f} s", flush=True)
-    rec = torch.empty((n, 32), dtype=torch.uint8, device=d)
-    ext = torch.zeros((n, 12), dtype=torch.uint8, device=d)
+    rec = torch.empty((n, 16), dtype=torch.uint8, device=d)
+    ext = torch.empty((2, n, 16), dtype=torch.uint8, device=d)
     zp.batch.parse_batch(arena, offs, lens, rec, ext, check=False)
     s = torch.cuda.current_stream()
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
@@ -48,7 +48,7 @@ def main():
     frames = [arena[int(o):int(o) + int(l)].cpu().numpy().tobytes() for o, l in zip(so, sl)]
     sa, sof, sle = pack(frames)
     want, wext = orc.parse_batch(sa, sof, sle)
-    got, gext = zp.batch.records_to_numpy(rec[idx], ext[idx])
+    got, gext = zp.batch.records_to_numpy(rec[idx], ext[:, idx])
     assert_same(got, gext, want, wext)
     print(f"max_size_check: OK (last offset {int(offs[-1].item()):,})", flush=True)
 

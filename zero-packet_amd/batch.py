@@ -3,7 +3,9 @@
     arena  uint8  [B]       frames packed anywhere in one buffer
     offs   int64  [n]       frame start offsets (read as uint64)
     lens   int32  [n]       frame lengths (read as uint32)
-    -> records uint8 [n, 32] (zp_record), optional inner_ext uint8 [n, 12]
+    -> records uint8 [n, 16] (zp_record), ext uint8 [2, n, 16] (zp_ext_offsets:
+       [0] the outer ipv6 extension chains, [1] the ip_in_ip ones; an entry
+       is valid where the record's ZP_F_EXT / ZP_F_INNER_EXT bit is set)
 
 parse_batch() enqueues the HIP kernel on torch's current stream of the
 tensors' device (zp_parse_batch_device). No CPU fallback: non-CUDA tensors or
@@ -15,7 +17,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .records import EXT_DTYPE, RECORD_DTYPE
+from .records import EXT_BYTES, EXT_DTYPE, RECORD_BYTES, RECORD_DTYPE
 
 CONFIGS = {"c1": 1, "c2": 2, "c3": 3, "c4": 4, "c5": 5}
 SEED = 0x5EED2025
@@ -69,22 +71,30 @@ def check_batch(arena, offs, lens, outs=(), bounds=True):
             raise ValueError(f"frame ends at byte {hi}, past the arena ({arena.numel()} bytes)")
 
 
-def parse_batch(arena, offs, lens, records=None, inner_ext=None, stream=None, check=True):
-    """Parses every frame; returns (records, inner_ext) as uint8 device tensors.
+def alloc_outputs(n, device, records=None, ext=None):
+    """records uint8 [n, 16] and ext uint8 [2, n, 16] device tensors (the ones
+    given are kept)."""
+    if records is None:
+        records = torch.empty((n, RECORD_BYTES), dtype=torch.uint8, device=device)
+    if ext is None:
+        ext = torch.empty((2, n, EXT_BYTES), dtype=torch.uint8, device=device)
+    return records, ext
+
+
+def parse_batch(arena, offs, lens, records=None, ext=None, stream=None, check=True):
+    """Parses every frame; returns (records, ext) as uint8 device tensors.
     check=False skips the descriptor bounds reduction (check_batch) for callers
     that validated the batch already; shapes and devices are always checked."""
     n = offs.numel()
     dev = arena.device
-    if records is None and arena.is_cuda:
-        records = torch.empty((n, 32), dtype=torch.uint8, device=dev)
-    if inner_ext is None and arena.is_cuda:
-        inner_ext = torch.zeros((n, 12), dtype=torch.uint8, device=dev)
-    check_batch(arena, offs, lens, ((records, 32), (inner_ext, 12)), bounds=check)
+    if arena.is_cuda:
+        records, ext = alloc_outputs(n, dev, records, ext)
+    check_batch(arena, offs, lens, ((records, RECORD_BYTES), (ext, 2 * EXT_BYTES)), bounds=check)
     s = ctypes.c_void_p(stream) if stream is not None else _stream_ptr(dev)
     rc = _lib.hip().zp_parse_batch_device(arena.data_ptr(), offs.data_ptr(), lens.data_ptr(), n,
-                                          records.data_ptr(), inner_ext.data_ptr(), s)
+                                          records.data_ptr(), ext.data_ptr(), s)
     _lib.check(rc, "zp_parse_batch_device")
-    return records, inner_ext
+    return records, ext
 
 
 def generate(config, n, seed=SEED, first=0, device="cuda", pad=64):
@@ -122,11 +132,12 @@ def generate_host(config, n, seed=SEED, first=0, nthreads=0, pad=64):
     return arena, offs, lens
 
 
-def records_to_numpy(records, inner_ext=None):
-    """uint8 [n,32] (device or host) -> structured numpy (RECORD_DTYPE)."""
+def records_to_numpy(records, ext=None):
+    """uint8 [n, 16] (device or host) -> structured numpy (RECORD_DTYPE) [n];
+    with ext (uint8 [2, n, 16]) also the chains as EXT_DTYPE [2, n]."""
     r = records.cpu().numpy() if isinstance(records, torch.Tensor) else records
     rec = np.ascontiguousarray(r).view(RECORD_DTYPE).reshape(-1)
-    if inner_ext is None:
+    if ext is None:
         return rec
-    e = inner_ext.cpu().numpy() if isinstance(inner_ext, torch.Tensor) else inner_ext
-    return rec, np.ascontiguousarray(e).view(EXT_DTYPE).reshape(-1)
+    e = ext.cpu().numpy() if isinstance(ext, torch.Tensor) else ext
+    return rec, np.ascontiguousarray(e).view(EXT_DTYPE).reshape(2, -1)

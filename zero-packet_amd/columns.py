@@ -14,7 +14,8 @@ import numpy as np
 import torch
 
 from . import _lib
-from .batch import check_batch
+from .batch import alloc_outputs, check_batch
+from .records import EXT_BYTES, RECORD_BYTES
 
 # (name, torch dtype, elements per frame) in zp_col order.
 COLUMNS = [
@@ -55,7 +56,7 @@ def extract(arena, offs, lens, records, names=None, out=None, stream=None, check
         if not t.is_cuda:
             raise RuntimeError("columns.extract needs device tensors (no CPU fallback)")
     n = offs.numel()
-    check_batch(arena, offs, lens, ((records, 32),), bounds=check)
+    check_batch(arena, offs, lens, ((records, RECORD_BYTES),), bounds=check)
     names = list(names) if names is not None else NAMES
     out = dict(out or {})
     ptrs = (ctypes.c_void_p * len(COLUMNS))()
@@ -73,19 +74,16 @@ def extract(arena, offs, lens, records, names=None, out=None, stream=None, check
     return {k: out[k] for k in names}
 
 
-def parse_with_columns(arena, offs, lens, names=None, records=None, inner_ext=None, out=None,
+def parse_with_columns(arena, offs, lens, names=None, records=None, ext=None, out=None,
                        stream=None, check=True):
     """zp_parse_batch_columns_device: records and the requested columns in one
-    pass over the frames. Returns (records, inner_ext, {name: tensor})."""
+    pass over the frames. Returns (records, ext, {name: tensor})."""
     for t in (arena, offs, lens):
         if not t.is_cuda:
             raise RuntimeError("columns.parse_with_columns needs device tensors (no CPU fallback)")
     n = offs.numel()
     d = arena.device
-    if records is None:
-        records = torch.empty((n, 32), dtype=torch.uint8, device=d)
-    if inner_ext is None:
-        inner_ext = torch.zeros((n, 12), dtype=torch.uint8, device=d)
+    records, ext = alloc_outputs(n, d, records, ext)
     names = list(names) if names is not None else NAMES
     out = dict(out or {})
     ptrs = (ctypes.c_void_p * len(COLUMNS))()
@@ -93,12 +91,12 @@ def parse_with_columns(arena, offs, lens, names=None, records=None, inner_ext=No
         if name not in out:
             out[name] = _alloc(name, n, d)
         ptrs[INDEX[name]] = out[name].data_ptr()
-    check_batch(arena, offs, lens, [(records, 32), (inner_ext, 12)] +
+    check_batch(arena, offs, lens, [(records, RECORD_BYTES), (ext, 2 * EXT_BYTES)] +
                 [(out[k], width(k)) for k in names], bounds=check)
     s = ctypes.c_void_p(stream) if stream is not None else \
         ctypes.c_void_p(torch.cuda.current_stream(d).cuda_stream)
     rc = _lib.hip().zp_parse_batch_columns_device(arena.data_ptr(), offs.data_ptr(),
                                                   lens.data_ptr(), n, records.data_ptr(),
-                                                  inner_ext.data_ptr(), ptrs, s)
+                                                  ext.data_ptr(), ptrs, s)
     _lib.check(rc, "zp_parse_batch_columns_device")
-    return records, inner_ext, {k: out[k] for k in names}
+    return records, ext, {k: out[k] for k in names}

@@ -113,12 +113,12 @@ extern "C" zp_ctx* zp_ctx_create(int device, uint64_t chunk_bytes) {
         TRY(hipMalloc(&c->d_offs[k], c->chunk_pkts * sizeof(uint64_t)));
         TRY(hipMalloc(&c->d_lens[k], c->chunk_pkts * sizeof(uint32_t)));
         TRY(hipMalloc(&c->d_rec[k], c->chunk_pkts * sizeof(zp_record)));
-        TRY(hipMalloc(&c->d_ext[k], c->chunk_pkts * sizeof(zp_ext_offsets)));
+        TRY(hipMalloc(&c->d_ext[k], 2 * c->chunk_pkts * sizeof(zp_ext_offsets)));
         TRY(hipHostMalloc(&c->h_arena[k], chunk_bytes + 64, hipHostMallocDefault));
         TRY(hipHostMalloc(&c->h_offs[k], c->chunk_pkts * sizeof(uint64_t), hipHostMallocDefault));
         TRY(hipHostMalloc(&c->h_lens[k], c->chunk_pkts * sizeof(uint32_t), hipHostMallocDefault));
         TRY(hipHostMalloc(&c->h_rec[k], c->chunk_pkts * sizeof(zp_record), hipHostMallocDefault));
-        TRY(hipHostMalloc(&c->h_ext[k], c->chunk_pkts * sizeof(zp_ext_offsets), hipHostMallocDefault));
+        TRY(hipHostMalloc(&c->h_ext[k], 2 * c->chunk_pkts * sizeof(zp_ext_offsets), hipHostMallocDefault));
     }
     (void)hipSetDevice(prev);
     return c;
@@ -137,9 +137,12 @@ static bool is_pinned(const void* p) {
 
 struct Pending { uint64_t i, j; bool live; };
 
-// Copies a finished slot's results to the user arrays.
-static int drain(zp_ctx* c, int k, Pending& pd, zp_record* recs, zp_ext_offsets* ext,
-                 bool rec_direct) {
+// Copies a finished slot's results to the user arrays: the outer and the
+// ip_in_ip chains go to xo[i] / xi[i] (the two halves of the caller's 2n-entry
+// ext array); the slot's device buffer holds the chunk's m frames as one
+// 2m-entry ext array ([0, m) outer, [m, 2m) ip_in_ip).
+static int drain(zp_ctx* c, int k, Pending& pd, zp_record* recs, zp_ext_offsets* xo,
+                 zp_ext_offsets* xi, bool rec_direct) {
     if (!pd.live) return 0;
     hipError_t e = hipEventSynchronize(c->ev[k]);
     if (e != hipSuccess) {
@@ -148,9 +151,12 @@ static int drain(zp_ctx* c, int k, Pending& pd, zp_record* recs, zp_ext_offsets*
     }
     uint64_t m = pd.j - pd.i;
     if (!rec_direct) memcpy(recs + pd.i, c->h_rec[k], m * sizeof(zp_record));
-    if (ext) {
-        for (uint64_t q = 0; q < m; ++q)
-            if (recs[pd.i + q].flags & ZP_F_INNER_EXT) ext[pd.i + q] = c->h_ext[k][q];
+    if (xo) {
+        for (uint64_t q = 0; q < m; ++q) {
+            const uint32_t f = recs[pd.i + q].flags;
+            if (f & ZP_F_EXT) xo[pd.i + q] = c->h_ext[k][q];
+            if (f & ZP_F_INNER_EXT) xi[pd.i + q] = c->h_ext[k][m + q];
+        }
     }
     pd.live = false;
     return 0;
@@ -159,9 +165,12 @@ static int drain(zp_ctx* c, int k, Pending& pd, zp_record* recs, zp_ext_offsets*
 extern "C" int zp_parse_batch_device(const uint8_t*, const uint64_t*, const uint32_t*, uint64_t,
                                      zp_record*, zp_ext_offsets*, void*);
 
-extern "C" int zp_parse_batch_host(zp_ctx* c, const uint8_t* arena, uint64_t arena_bytes,
-                                   const uint64_t* offs, const uint32_t* lens, uint64_t n,
-                                   zp_record* recs, zp_ext_offsets* ext) {
+// The host path over frames [0, n) with the chains going to xo / xi (both
+// NULL: chains dropped).
+static int parse_host(zp_ctx* c, const uint8_t* arena, uint64_t arena_bytes,
+                      const uint64_t* offs, const uint32_t* lens, uint64_t n,
+                      zp_record* recs, zp_ext_offsets* xo, zp_ext_offsets* xi) {
+    zp_ext_offsets* ext = xo;
     if (!c || (n && (!arena || !offs || !lens || !recs))) return -1;
     if (n == 0) return 0;
     int prev = 0;
@@ -196,7 +205,7 @@ extern "C" int zp_parse_batch_host(zp_ctx* c, const uint8_t* arena, uint64_t are
             if (h2 - l2 > c->chunk_bytes || (arena_bytes && h2 > arena_bytes)) break;
             lo = l2; hi = h2; ++j;
         }
-        if ((rc = drain(c, k, pd[k], recs, ext, rec_direct)) != 0) break;
+        if ((rc = drain(c, k, pd[k], recs, xo, xi, rec_direct)) != 0) break;
         uint64_t m = j - i;
         for (uint64_t q = 0; q < m; ++q) {
             c->h_offs[k][q] = offs[i + q] - lo;
@@ -221,7 +230,7 @@ extern "C" int zp_parse_batch_host(zp_ctx* c, const uint8_t* arena, uint64_t are
         e = hipMemcpyAsync(rec_direct ? (void*)(recs + i) : (void*)c->h_rec[k], c->d_rec[k],
                            m * sizeof(zp_record), hipMemcpyDeviceToHost, s);
         if (e == hipSuccess && ext)
-            e = hipMemcpyAsync(c->h_ext[k], c->d_ext[k], m * sizeof(zp_ext_offsets),
+            e = hipMemcpyAsync(c->h_ext[k], c->d_ext[k], 2 * m * sizeof(zp_ext_offsets),
                                hipMemcpyDeviceToHost, s);
         if (e == hipSuccess) e = hipEventRecord(c->ev[k], s);
         if (e != hipSuccess) {
@@ -234,21 +243,27 @@ extern "C" int zp_parse_batch_host(zp_ctx* c, const uint8_t* arena, uint64_t are
         k = (k + 1) % SLOTS;
     }
     for (int q = 0; q < SLOTS; ++q) {
-        int r2 = drain(c, (k + q) % SLOTS, pd[(k + q) % SLOTS], recs, ext, rec_direct);
+        int r2 = drain(c, (k + q) % SLOTS, pd[(k + q) % SLOTS], recs, xo, xi, rec_direct);
         if (!rc) rc = r2;
     }
     (void)hipSetDevice(prev);
     return rc;
 }
 
+extern "C" int zp_parse_batch_host(zp_ctx* c, const uint8_t* arena, uint64_t arena_bytes,
+                                   const uint64_t* offs, const uint32_t* lens, uint64_t n,
+                                   zp_record* recs, zp_ext_offsets* ext) {
+    return parse_host(c, arena, arena_bytes, offs, lens, n, recs, ext, ext ? ext + n : NULL);
+}
+
 extern "C" int zp_parse_one(zp_ctx* c, const uint8_t* frame, uint64_t len,
-                            zp_record* record, zp_ext_offsets* inner_ext) {
+                            zp_record* record, zp_ext_offsets* ext) {
     uint64_t off = 0;
     uint32_t l = (uint32_t)len;
     if (len > 0xFFFFFFFFull) return -1;
     static const uint8_t empty[16] = {0};
     if (!frame) frame = empty;
-    int rc = zp_parse_batch_host(c, frame, len, &off, &l, 1, record, inner_ext);
+    int rc = zp_parse_batch_host(c, frame, len, &off, &l, 1, record, ext);
     if (rc) return rc;
     return record->err;
 }
@@ -268,15 +283,16 @@ struct MultiJob {
     const uint32_t* lens;
     uint64_t n;
     zp_record* recs;
-    zp_ext_offsets* ext;
+    zp_ext_offsets* xo;
+    zp_ext_offsets* xi;
     int rc;
     char err[ERRBUF_LEN];
 };
 
 static void* multi_worker(void* p) {
     MultiJob* j = (MultiJob*)p;
-    j->rc = zp_parse_batch_host(j->ctx, j->arena, j->arena_bytes, j->offs, j->lens, j->n,
-                                j->recs, j->ext);
+    j->rc = parse_host(j->ctx, j->arena, j->arena_bytes, j->offs, j->lens, j->n, j->recs,
+                       j->xo, j->xi);
     if (j->rc) snprintf(j->err, ERRBUF_LEN, "%s", g_ctx_error);
     return NULL;
 }
@@ -308,7 +324,7 @@ extern "C" int zp_parse_batch_host_multi(zp_ctx* const* ctxs, int nctx, const ui
                               : (uint64_t)((unsigned __int128)total * (unsigned)(d + 1) / (unsigned)nctx);
         while (i < n && acc < target) acc += lens[i++];
         jobs[d] = MultiJob{ctxs[d], arena, arena_bytes, offs + lo, lens + lo, i - lo, recs + lo,
-                           ext ? ext + lo : NULL, 0, {0}};
+                           ext ? ext + lo : NULL, ext ? ext + n + lo : NULL, 0, {0}};
     }
     int rc = 0;
     for (int d = 0; d < nctx; ++d) {

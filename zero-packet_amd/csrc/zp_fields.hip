@@ -93,8 +93,9 @@ zp_columns_kernel(const uint8_t* __restrict__ arena, const uint64_t* __restrict_
     const uint4* rp = (const uint4*)(recs + i);
     zp_record r;
     {
-        uint4 q[2] = {rp[0], rp[1]};
-        __builtin_memcpy(&r, q, sizeof r);
+        const uint4 q = rp[0];
+        static_assert(sizeof(zp_record) == sizeof(uint4), "one 16-B load per record");
+        __builtin_memcpy(&r, &q, sizeof r);
     }
     const bool ok = live && r.err == 0 && (r.flags & ZP_F_ETHERNET);
     const uint32_t len = ok ? lens[i] : 0u;

@@ -15,7 +15,7 @@
 //      and cut into items of 64 chunks; see "The stream" below); per-frame
 //      sums by running prefix; header windows and last chunks to LDS;
 //   3. lane-per-frame header walk from the LDS window;
-//   4. checksum verdict, 32-B record store.
+//   4. checksum verdict, 16-B record store (+ extension chains, if any).
 // Checksum arithmetic. The reference verifies S = acc + sum of big-endian
 // 16-bit words (u32), valid iff !fold(S) as u16 == 0 (checksum.rs:5-35),
 // i.e. S != 0 and S == 0 (mod 65535). We sum little-endian 16-bit words at
@@ -325,7 +325,8 @@ __device__ bool csum_ok_exact(const uint8_t* g, uint32_t lo, uint32_t hi, uint32
 // --------------------------------------------------------------------------
 struct Walk {
     zp_record rec;
-    zp_ext_offsets inner;
+    zp_ext_offsets outer;    // ipv6 extension chain (valid iff ZP_F_EXT)
+    zp_ext_offsets inner;    // ip_in_ip IPv6 chain (valid iff ZP_F_INNER_EXT)
     uint32_t acc;        // exact pseudo-header accumulator of the innermost IP
     uint32_t l4;         // L4 start (frame offset) when a checksum is pending
     uint8_t pending;     // 1 = L4 checksum still to verify
@@ -451,8 +452,8 @@ __device__ __forceinline__ void walk_frame(FrameView& f, Walk& w) {
                         r.final_nh = (uint8_t)proto;
                         if (pres) {
                             r.flags |= ZP_F_EXT | (pres << 12);
-                            r.ext_len = (uint16_t)tot;
-                            for (int k = 0; k < 6; ++k) r.ext_off[k] = eo[k];
+                            w.outer.len = (uint16_t)tot;
+                            for (int k = 0; k < 6; ++k) w.outer.off[k] = eo[k];
                         }
                     } else if (level == 1) {
                         r.flags |= ZP_F_IP_IN_IP | ZP_F_IP_IN_IP_V6;
@@ -460,7 +461,7 @@ __device__ __forceinline__ void walk_frame(FrameView& f, Walk& w) {
                         r.inner_final_nh = (uint8_t)proto;
                         if (pres) {
                             r.flags |= ZP_F_INNER_EXT | (pres << 18);
-                            r.inner_ext_len = (uint16_t)tot;
+                            w.inner.len = (uint16_t)tot;
                             for (int k = 0; k < 6; ++k) w.inner.off[k] = eo[k];
                         }
                     }
@@ -548,7 +549,7 @@ struct ViewReader {
 template <bool COLS>
 __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, WaveLds& lds,
                                             zp_record* __restrict__ records,
-                                            zp_ext_offsets* __restrict__ inner_ext,
+                                            zp_ext_offsets* __restrict__ ext,
                                             const ColPtrs& cols) {
     uint4* tail = &lds.win[ZP_WIN_CH * 64];
     const uint8_t* g = (const uint8_t*)s.ga;
@@ -563,6 +564,7 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
     fv.xi = ~0u;
     Walk w;
     w.rec = zp_record{};
+    w.outer = zp_ext_offsets{};
     w.inner = zp_ext_offsets{};
 #ifdef ZP_ABL_FAKE_WALK
     w.pending = s.live && s.len >= 64;
@@ -597,22 +599,31 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
             rec.err = (uint8_t)(w.v6 ? ZP_ERR_IPV6_L4_CHECKSUM : ZP_ERR_IPV4_L4_CHECKSUM);
         }
     }
-    uint4 q2[2];
-    memcpy(q2, &rec, sizeof rec);
+    static_assert(sizeof(zp_record) == 16 && sizeof(zp_ext_offsets) == 16, "16-B records");
     const uint64_t p = s.tile * 64 + lane;
 #ifdef ZP_ABL_NOREC
     if (rec.flags == 0xDEADBEEFu)                       // timing ablation: no stores
 #endif
     {
-        // Nontemporal stores: the records are write-once output. The record
-        // writes, not their 4 % of the bytes, are what makes the kernel
-        // sensitive to the arena's placement (without them every placement
-        // runs in 1.95 ms); nt takes 6-7 % off on every placement (r01).
-        zp_u32x4* dst = (zp_u32x4*)(records + p);
-        __builtin_nontemporal_store(zp_u32x4{q2[0].x, q2[0].y, q2[0].z, q2[0].w}, dst);
-        __builtin_nontemporal_store(zp_u32x4{q2[1].x, q2[1].y, q2[1].z, q2[1].w}, dst + 1);
+        // One nontemporal 16-B store per frame: 1 KiB of whole lines per wave
+        // instruction. The record writes, not their share of the bytes, are
+        // what makes the kernel sensitive to the placement of the arena and
+        // the records (without them every placement runs in 1.95 ms); nt took
+        // 6-7 % off on every placement, and 16-B records (v2) 4-6 % more
+        // than 32-B ones.
+        uint4 q;
+        memcpy(&q, &rec, sizeof rec);
+        __builtin_nontemporal_store(zp_u32x4{q.x, q.y, q.z, q.w}, (zp_u32x4*)(records + p));
     }
-    if (inner_ext && (rec.flags & ZP_F_INNER_EXT)) inner_ext[p] = w.inner;
+    if (ext) {
+        // The extension chains: a wave with many chains writes the entries of
+        // all its frames (whole lines, zero where absent), one with a few
+        // only those of its chains.
+        const bool ho = rec.flags & ZP_F_EXT, hi = rec.flags & ZP_F_INNER_EXT;
+        const uint64_t mo = __ballot(ho), mi = __ballot(hi);
+        if (mo && (ho || __builtin_popcountll(mo) >= 16)) ext[p] = ho ? w.outer : zp_ext_offsets{};
+        if (mi && (hi || __builtin_popcountll(mi) >= 16)) ext[n + p] = hi ? w.inner : zp_ext_offsets{};
+    }
     if (COLS) {
         ViewReader rdr{fv};
         emit_columns(rdr, rec, rec.err == 0 && (rec.flags & ZP_F_ETHERNET), s.len, p, cols);
@@ -637,7 +648,7 @@ __device__ __forceinline__ void parse_tiles(const uint8_t* __restrict__ arena,
                                             const uint64_t* __restrict__ offs,
                                             const uint32_t* __restrict__ lens, uint64_t n,
                                             zp_record* __restrict__ records,
-                                            zp_ext_offsets* __restrict__ inner_ext,
+                                            zp_ext_offsets* __restrict__ ext,
                                             const ColPtrs& cols) {
     __shared__ WaveLds lds_all[ZP_WAVES];
     const int lane = threadIdx.x & 63;
@@ -647,8 +658,21 @@ __device__ __forceinline__ void parse_tiles(const uint8_t* __restrict__ arena,
     uint4* win = &lds.win[0];
     uint4* tail = &lds.win[ZP_WIN_CH * 64];
     // ZP_K consecutive tiles per wave (one contiguous band of the arena)
+#ifdef ZP_SEG
+    // A/B: the grid's blocks interleaved over ZP_SEG contiguous segments of the
+    // batch (a bijection), so the resident waves stream ZP_SEG bands at once.
+    uint64_t blk = blockIdx.x;
+    {
+        const uint64_t B = gridDim.x, S = ZP_SEG, q = B / S, r = B % S;
+        const uint64_t s = blk < S * q ? blk % S : blk - S * q;
+        const uint64_t i = blk < S * q ? blk / S : q;
+        blk = s * q + (s < r ? s : r) + i;
+    }
+#else
+    const uint64_t blk = blockIdx.x;
+#endif
     for (uint32_t k = 0; k < ZP_K; ++k) {
-        const uint64_t t = ((uint64_t)blockIdx.x * ZP_WAVES + wid) * ZP_K + k;
+        const uint64_t t = (blk * ZP_WAVES + wid) * ZP_K + k;
         if (t * 64 >= n) return;                   // wave-uniform
 #ifdef ZP_STAMPS
         const uint64_t wave_id = t;
@@ -682,7 +706,7 @@ __device__ __forceinline__ void parse_tiles(const uint8_t* __restrict__ arena,
         __builtin_amdgcn_s_setprio(0);             // walk at priority 0 ...
 #endif
         STAMP(3);
-        tile_finish<COLS>(s, n, lane, lds, records, inner_ext, cols);
+        tile_finish<COLS>(s, n, lane, lds, records, ext, cols);
         STAMP(4);
     }
 }
@@ -690,23 +714,23 @@ __device__ __forceinline__ void parse_tiles(const uint8_t* __restrict__ arena,
 __global__ void ZP_KATTR
 zp_parse_kernel(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs,
                 const uint32_t* __restrict__ lens, uint64_t n,
-                zp_record* __restrict__ records, zp_ext_offsets* __restrict__ inner_ext) {
+                zp_record* __restrict__ records, zp_ext_offsets* __restrict__ ext) {
     const ColPtrs none{};
-    parse_tiles<false>(arena, offs, lens, n, records, inner_ext, none);
+    parse_tiles<false>(arena, offs, lens, n, records, ext, none);
 }
 
 // Parse + column views in one pass (zp_parse_batch_columns_device).
 __global__ void ZP_KATTR_COLS
 zp_parse_columns_kernel(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs,
                         const uint32_t* __restrict__ lens, uint64_t n,
-                        zp_record* __restrict__ records, zp_ext_offsets* __restrict__ inner_ext,
+                        zp_record* __restrict__ records, zp_ext_offsets* __restrict__ ext,
                         ColPtrs cols) {
-    parse_tiles<true>(arena, offs, lens, n, records, inner_ext, cols);
+    parse_tiles<true>(arena, offs, lens, n, records, ext, cols);
 }
 
 extern "C" int zp_parse_batch_device(const uint8_t* arena, const uint64_t* offs,
                                      const uint32_t* lens, uint64_t n,
-                                     zp_record* records, zp_ext_offsets* inner_ext,
+                                     zp_record* records, zp_ext_offsets* ext,
                                      void* stream) {
     if (n == 0) return 0;
     if (!arena || !offs || !lens || !records) {
@@ -720,7 +744,7 @@ extern "C" int zp_parse_batch_device(const uint8_t* arena, const uint64_t* offs,
         return -1;
     }
     hipLaunchKernelGGL(zp_parse_kernel, dim3((unsigned)blocks), dim3(64 * ZP_WAVES), 0,
-                       (hipStream_t)stream, arena, offs, lens, n, records, inner_ext);
+                       (hipStream_t)stream, arena, offs, lens, n, records, ext);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) { set_err("zp_parse_kernel launch", e); return -2; }
     return 0;
@@ -728,7 +752,7 @@ extern "C" int zp_parse_batch_device(const uint8_t* arena, const uint64_t* offs,
 
 extern "C" int zp_parse_batch_columns_device(const uint8_t* arena, const uint64_t* offs,
                                              const uint32_t* lens, uint64_t n,
-                                             zp_record* records, zp_ext_offsets* inner_ext,
+                                             zp_record* records, zp_ext_offsets* ext,
                                              void* const* cols, void* stream) {
     if (n == 0) return 0;
     if (!arena || !offs || !lens || !records || !cols) {
@@ -744,7 +768,7 @@ extern "C" int zp_parse_batch_columns_device(const uint8_t* arena, const uint64_
         return -1;
     }
     hipLaunchKernelGGL(zp_parse_columns_kernel, dim3((unsigned)blocks), dim3(64 * ZP_WAVES), 0,
-                       (hipStream_t)stream, arena, offs, lens, n, records, inner_ext, c);
+                       (hipStream_t)stream, arena, offs, lens, n, records, ext, c);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) { set_err("zp_parse_columns_kernel launch", e); return -2; }
     return 0;

@@ -87,7 +87,7 @@ static void fill_view(const zp_ring* r, uint32_t k, zp_ring_slot* out) {
     out->arena_cap = r->slot_bytes;
     out->frames_cap = r->slot_frames;
     out->records = s.h_rec;
-    out->inner_ext = s.h_ext;
+    out->ext = s.h_ext;
     out->n = s.n;
     out->seq = s.seq;
 }
@@ -152,12 +152,12 @@ extern "C" zp_ring* zp_ring_create(int device, uint32_t nslots, uint64_t slot_by
         RTRY(hipHostMalloc(&s.h_offs, slot_frames * sizeof(uint64_t), hipHostMallocDefault));
         RTRY(hipHostMalloc(&s.h_lens, slot_frames * sizeof(uint32_t), hipHostMallocDefault));
         RTRY(hipHostMalloc(&s.h_rec, slot_frames * sizeof(zp_record), hipHostMallocDefault));
-        RTRY(hipHostMalloc(&s.h_ext, slot_frames * sizeof(zp_ext_offsets), hipHostMallocDefault));
+        RTRY(hipHostMalloc(&s.h_ext, 2 * slot_frames * sizeof(zp_ext_offsets), hipHostMallocDefault));
         RTRY(hipMalloc(&s.d_arena, slot_bytes + 64));
         RTRY(hipMalloc(&s.d_offs, slot_frames * sizeof(uint64_t)));
         RTRY(hipMalloc(&s.d_lens, slot_frames * sizeof(uint32_t)));
         RTRY(hipMalloc(&s.d_rec, slot_frames * sizeof(zp_record)));
-        RTRY(hipMalloc(&s.d_ext, slot_frames * sizeof(zp_ext_offsets)));
+        RTRY(hipMalloc(&s.d_ext, 2 * slot_frames * sizeof(zp_ext_offsets)));
     }
     (void)hipSetDevice(prev);
     return r;
@@ -229,7 +229,7 @@ extern "C" int zp_ring_submit(zp_ring* r, int32_t id, uint64_t n) {
         if (e == hipSuccess && rc == 0)
             e = hipMemcpyAsync(s.h_rec, s.d_rec, n * sizeof(zp_record), hipMemcpyDeviceToHost, s.s);
         if (e == hipSuccess && rc == 0)
-            e = hipMemcpyAsync(s.h_ext, s.d_ext, n * sizeof(zp_ext_offsets),
+            e = hipMemcpyAsync(s.h_ext, s.d_ext, 2 * n * sizeof(zp_ext_offsets),
                                hipMemcpyDeviceToHost, s.s);
     }
     if (e == hipSuccess && rc == 0) e = hipEventRecord(s.done, s.s);

@@ -391,8 +391,10 @@ class PacketParser:
             setattr(self, f, None)
 
     @classmethod
-    def from_record(cls, frame, rec, inner_ext=None):
+    def from_record(cls, frame, rec, ext=None):
         """Rebuilds the parser of `frame` from its zp_record (no re-parse).
+        ext: the frame's two zp_ext_offsets entries (outer ipv6 chain,
+        ip_in_ip chain; EXT_DTYPE [2]), needed when the record flags a chain.
         Raises ZeroPacketError when the record holds an error."""
         frame = bytes(frame)
         err = int(rec["err"])
@@ -400,6 +402,8 @@ class PacketParser:
             raise ZeroPacketError(_lib.hip().zp_err_str(err).decode() if _lib_available()
                                   else f"zp_err {err}", err)
         flags = int(rec["flags"])
+        if flags & (F_EXT | F_INNER_EXT) and ext is None:
+            raise ValueError("the record flags an IPv6 extension chain: pass its ext entries")
         p = cls()
         hl = int(rec["eth_len"])
         if flags & F_ETHERNET:
@@ -411,19 +415,19 @@ class PacketParser:
         if flags & F_IPV6:
             eh = None
             if flags & F_EXT:
-                eh = _ext_from(frame, hl + 40, flags, 12, rec["ext_off"], rec["ext_len"],
-                               rec["final_nh"])
-            p.ipv6 = IPv6Reader(frame[hl:], eh, int(rec["ext_len"]) if eh else 0)
+                x = ext[0]
+                eh = _ext_from(frame, hl + 40, flags, 12, x["off"], x["len"], rec["final_nh"])
+            p.ipv6 = IPv6Reader(frame[hl:], eh, int(ext[0]["len"]) if eh else 0)
         if flags & F_IP_IN_IP:
             io = int(rec["inner_off"])
             if flags & F_IP_IN_IP_V6:
                 eh = None
                 if flags & F_INNER_EXT:
-                    offs = inner_ext["off"] if inner_ext is not None else [0] * 6
-                    eh = _ext_from(frame, io + 40, flags, 18, offs, rec["inner_ext_len"],
+                    x = ext[1]
+                    eh = _ext_from(frame, io + 40, flags, 18, x["off"], x["len"],
                                    rec["inner_final_nh"])
                 p.ip_in_ip = IpInIp("ipv6", IPv6Reader(frame[io:], eh,
-                                                       int(rec["inner_ext_len"]) if eh else 0))
+                                                       int(ext[1]["len"]) if eh else 0))
             else:
                 p.ip_in_ip = IpInIp("ipv4", IPv4Reader(frame[io:]))
         l4 = int(rec["l4_off"])
@@ -447,7 +451,7 @@ class PacketParser:
         """PacketParser::parse (parser.rs:53) through the GPU path."""
         frame = bytes(frame)
         rec = np.zeros(1, RECORD_DTYPE)
-        ext = np.zeros(1, EXT_DTYPE)
+        ext = np.zeros(2, EXT_DTYPE)
         buf = ctypes.create_string_buffer(frame, len(frame) or 1)
         # The shared zp_ctx (pinned staging, device buffers, streams) serves one
         # call at a time; ctypes releases the GIL, so callers on other threads
@@ -456,7 +460,7 @@ class PacketParser:
             rc = _lib.hip().zp_parse_one(_default_ctx(), ctypes.addressof(buf), len(frame),
                                          rec.ctypes.data, ext.ctypes.data)
         _lib.check(rc, "zp_parse_one")
-        return cls.from_record(frame, rec[0], ext[0])
+        return cls.from_record(frame, rec[0], ext)
 
 
 def _lib_available():

@@ -4,11 +4,24 @@ import numpy as np
 RECORD_DTYPE = np.dtype([
     ("flags", "<u4"), ("err", "u1"), ("eth_len", "u1"), ("final_nh", "u1"),
     ("inner_final_nh", "u1"), ("inner_off", "<u4"), ("l4_off", "<u4"),
-    ("ext_len", "<u2"), ("ext_off", "<u2", (6,)), ("inner_ext_len", "<u2"),
 ])
-assert RECORD_DTYPE.itemsize == 32
-EXT_DTYPE = np.dtype([("off", "<u2", (6,))])
-assert EXT_DTYPE.itemsize == 12
+assert RECORD_DTYPE.itemsize == 16
+# One IPv6 extension chain (zp_ext_offsets). A batch of n frames has 2n of
+# them: [0, n) the outer ipv6 chains, [n, 2n) the ip_in_ip ones; numpy views
+# them as shape (2, n).
+EXT_DTYPE = np.dtype([("len", "<u2"), ("off", "<u2", (6,)), ("reserved", "<u2")])
+assert EXT_DTYPE.itemsize == 16
+RECORD_BYTES, EXT_BYTES = 16, 16
+
+
+def ext_match(got, want, rec):
+    """True when the chains the records flag are identical (other entries are
+    unspecified by the ABI). got/want: EXT_DTYPE (2, n); rec: RECORD_DTYPE (n,)."""
+    mo = (rec["flags"] & F_EXT) != 0
+    mi = (rec["flags"] & F_INNER_EXT) != 0
+    return (got[0][mo].tobytes() == want[0][mo].tobytes() and
+            got[1][mi].tobytes() == want[1][mi].tobytes())
+
 
 # Presence bits (zero_packet.h ZP_F_*).
 F_ETHERNET, F_ARP, F_IPV4, F_IPV6 = 1 << 0, 1 << 1, 1 << 2, 1 << 3

@@ -5,7 +5,7 @@
     ... fill s.arena / s.offs[:n] / s.lens[:n] (a NIC ring would DMA here) ...
     ring.submit(s, n)                  # H2D -> parse -> D2H, asynchronous
     d = ring.wait()                    # oldest submitted slot, results in host memory
-    use(d.records)                     # numpy RECORD_DTYPE [n]
+    use(d.records, d.ext)              # numpy RECORD_DTYPE [n], EXT_DTYPE [2, n]
     ring.release(d)
 
 Frames start in host memory (README.md:85-115 of the reference feeds one
@@ -31,7 +31,7 @@ class _SlotC(ctypes.Structure):
     _fields_ = [("id", ctypes.c_int32), ("arena", ctypes.c_void_p), ("offs", ctypes.c_void_p),
                 ("lens", ctypes.c_void_p), ("arena_cap", ctypes.c_uint64),
                 ("frames_cap", ctypes.c_uint64), ("records", ctypes.c_void_p),
-                ("inner_ext", ctypes.c_void_p), ("n", ctypes.c_uint64), ("seq", ctypes.c_uint64)]
+                ("ext", ctypes.c_void_p), ("n", ctypes.c_uint64), ("seq", ctypes.c_uint64)]
 
 
 def _np(ptr, dtype, count):
@@ -52,7 +52,7 @@ class Slot:
         self.offs = _np(c.offs, np.uint64, c.frames_cap)
         self.lens = _np(c.lens, np.uint32, c.frames_cap)
         self.records = _np(c.records, RECORD_DTYPE, c.n)
-        self.inner_ext = _np(c.inner_ext, EXT_DTYPE, c.n)
+        self.ext = _np(c.ext, EXT_DTYPE, 2 * c.n).reshape(2, -1)   # [0] outer, [1] ip_in_ip
 
 
 def _sigs(lib):
@@ -128,23 +128,24 @@ class Ring:
     def release(self, slot):
         _lib.check(self.lib.zp_ring_release(self.h, slot.id), "zp_ring_release")
 
-    def parse(self, arena, offs, lens, out=None, inner_ext=None):
+    def parse(self, arena, offs, lens, out=None, ext=None):
         """Runs a host batch through the ring: frames are copied into slots
         (cut at slot capacity), slots overlap in flight, records land in
-        `out` (numpy RECORD_DTYPE [n]). Returns (out, inner_ext)."""
+        `out` (numpy RECORD_DTYPE [n]), chains in `ext` (EXT_DTYPE [2, n]).
+        Returns (out, ext)."""
         arena = np.asarray(arena, np.uint8)
         offs = np.asarray(offs, np.uint64)
         lens = np.asarray(lens, np.uint32)
         n = len(offs)
         out = np.zeros(n, RECORD_DTYPE) if out is None else out
-        inner_ext = np.zeros(n, EXT_DTYPE) if inner_ext is None else inner_ext
+        ext = np.zeros((2, n), EXT_DTYPE) if ext is None else ext
         pending = []          # (first frame, count) per submitted slot, FIFO
 
         def drain_one():
             d = self.wait()
             i0, m = pending.pop(0)
             out[i0:i0 + m] = d.records
-            inner_ext[i0:i0 + m] = d.inner_ext
+            ext[:, i0:i0 + m] = d.ext
             self.release(d)
 
         ends = offs + lens
@@ -169,4 +170,4 @@ class Ring:
             i = j
         while pending:
             drain_one()
-        return out, inner_ext
+        return out, ext
