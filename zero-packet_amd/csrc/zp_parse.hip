@@ -414,11 +414,16 @@ __device__ __forceinline__ void walk_frame(FrameView& f, Walk& w) {
             if (rd16(f, hl + 6) > 2) { err = ZP_ERR_ARP_INVALID_OPER; goto done; }
             r.flags |= ZP_F_ARP;
         } else if (et == 0x0800 || et == 0x86DD) {
+            // The IP levels (parse_ipv4 / parse_ipv6 and their IP-in-IP
+            // recursion, parser.rs:73-107,134-135) first; the L4 reader and
+            // the checksum of the innermost level after the loop, so a wave
+            // whose frames end at different levels runs that code once
+            // (c5 -5 %).
             uint32_t pos = hl;
             bool v4 = et == 0x0800;
+            uint32_t proto, pp;
             for (uint32_t level = 0;; ++level) {
                 const uint32_t sl = len - pos;                        // slice length
-                uint32_t proto, pp;
                 if (v4) {                                             // parser.rs:188-212
                     if (sl < 20) { err = ZP_ERR_IPV4_TOO_SHORT; goto done; }
                     const uint32_t b0 = rd8(f, pos);
@@ -466,6 +471,11 @@ __device__ __forceinline__ void walk_frame(FrameView& f, Walk& w) {
                         }
                     }
                 }
+                if (proto != 4 && proto != 41) break;                 // parse_protocol :111-140
+                v4 = proto == 4;                                      // IP-in-IP recursion
+                pos = pp;
+            }
+            {
                 const uint32_t rem = len - pp;                        // parse_protocol :111-140
                 const bool tcp = proto == 6, udp = proto == 17, ic4 = proto == 1;
                 if (tcp || udp || ic4 || proto == 58) {
@@ -491,12 +501,8 @@ __device__ __forceinline__ void walk_frame(FrameView& f, Walk& w) {
                     else e = !icmpv6_type_ok(t >> 8) ? ZP_ERR_ICMPV6_TYPE : 0;
                     if (e) { err = e; goto done; }
                     r.flags |= tcp ? ZP_F_TCP : udp ? ZP_F_UDP : ic4 ? ZP_F_ICMPV4 : ZP_F_ICMPV6;
-                } else if (proto == 4 || proto == 41) {               // IP-in-IP recursion
-                    v4 = proto == 4;
-                    pos = pp;
-                    continue;
                 } else {
-                    break;                                            // unknown: Ok, no L4
+                    goto ip_done;                                     // unknown: Ok, no L4
                 }
                 // Pseudo-header of the innermost IP only (outer levels of an
                 // IP-in-IP chain never need one): parser.rs:316-333 (IPv4;
@@ -516,9 +522,9 @@ __device__ __forceinline__ void walk_frame(FrameView& f, Walk& w) {
                 w.pending = 1;
                 w.l4 = pp;
                 w.v6 = v4 ? 0 : 1;
-                break;
             }
         }
+    ip_done:
         r.flags |= ZP_F_ETHERNET;
     }
 done:
