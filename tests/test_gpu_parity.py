@@ -386,3 +386,44 @@ def test_parse_one_threads(zp, golden):
     for t in ts:
         t.join()
     assert not bad, bad[:5]
+
+
+def test_ext_null_and_sparse(zp):
+    """ext = NULL drops the chains only (records identical); with an ext array
+    the flagged chains match the oracle both where a wave holds many chains
+    (whole-wave writes) and where it holds one (that entry only); a sentinel
+    shows which entries a sparse wave leaves untouched."""
+    import ctypes
+    arena, offs, lens = zp.batch.generate("c4", 4096, device=dev())
+    ext_rich = arena.new_zeros((2, 4096, 16))
+    r1, _ = zp.batch.parse_batch(arena, offs, lens, ext=ext_rich)
+    r0 = torch.empty_like(r1)
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    assert zp._lib.hip().zp_parse_batch_device(arena.data_ptr(), offs.data_ptr(), lens.data_ptr(),
+                                               4096, r0.data_ptr(), None, s) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(r0, r1)
+    want, wext = orc.parse_batch(arena.cpu().numpy(), offs.cpu().numpy(), lens.cpu().numpy())
+    got, gext = zp.batch.records_to_numpy(r1, ext_rich)
+    assert_same(got, gext, want, wext)
+    # one IPv6 frame with a chain among IPv4 frames: a sparse wave
+    a3, o3, l3 = zp.batch.generate("c3", 127, device=dev())
+    frames = [a3[int(o):int(o) + int(l)].cpu().numpy().tobytes()
+              for o, l in zip(o3.cpu().numpy(), l3.cpu().numpy())]
+    k = int(((want["flags"] & zp.records.F_EXT) != 0).nonzero()[0][0])
+    o4 = offs.cpu().numpy()
+    frames.insert(70, arena[int(o4[k]):int(o4[k]) + int(lens[k])].cpu().numpy().tobytes())
+    a, o, l_ = pack(frames)
+    d = dev()
+    ta = torch.from_numpy(a).to(d)
+    to = torch.from_numpy(o.astype(np.int64)).to(d)
+    tl = torch.from_numpy(l_.astype(np.int32)).to(d)
+    ext = torch.full((2, 128, 16), 0xA5, dtype=torch.uint8, device=d)
+    r, _ = zp.batch.parse_batch(ta, to, tl, ext=ext)
+    want, wext = orc.parse_batch(a, o, l_)
+    got, gext = zp.batch.records_to_numpy(r, ext)
+    assert_same(got, gext, want, wext)
+    assert int(((want["flags"] & zp.records.F_EXT) != 0).sum()) == 1
+    e = ext.cpu().numpy()
+    untouched = [i for i in range(128) if i != 70]
+    assert (e[0, untouched] == 0xA5).all() and (e[1] == 0xA5).all()
