@@ -212,6 +212,21 @@ int zp_parse_one(zp_ctx* ctx, const uint8_t* frame, uint64_t len,
                  zp_record* record, zp_ext_offsets ext[2]);
 
 /* ------------------------------------------------------------------------- */
+/* Per-batch counters: frames per presence bit of          */
+/* zp_record.flags and frames per zp_err code, for monitoring a capture      */
+/* (protocol mix, error histogram) without copying the records to the host. */
+/* ------------------------------------------------------------------------- */
+#define ZP_STATS_FLAG_BITS 24                      /* flags bits 0-23 (ZP_F_*, slots) */
+#define ZP_STAT_FLAG(bit)  (bit)                   /* frames with flags bit `bit` set */
+#define ZP_STAT_ERR(code)  (ZP_STATS_FLAG_BITS + (code))  /* frames with err == code   */
+#define ZP_STATS_COUNT     (ZP_STATS_FLAG_BITS + ZP_ERR_COUNT)
+/* Adds the counts of records[0, n) into counts[ZP_STATS_COUNT] (device u64,
+ * zeroed by the caller; several batches accumulate). Enqueues on `stream`.
+ * The counts of several devices add up on the host (frames are independent).
+ * Returns 0 or negative on launch failure. */
+int zp_stats_device(const zp_record* records, uint64_t n, uint64_t* counts, void* stream);
+
+/* ------------------------------------------------------------------------- */
 /* Host-ring ingestion pipeline. Frames start in host */
 /* memory (a NIC ring / raw socket, README.md:85-115 of the reference). A     */
 /* ring holds `nslots` slots, each with pinned host buffers, device buffers   */

@@ -6,6 +6,7 @@ Import with importlib (the directory name has a hyphen):
   zp.batch.parse_batch(arena, offs, lens)   device-resident batch parse (HIP)
   zp.batch.generate(cfg, n)                  synthetic BASELINE configs on the GPU
   zp.columns.extract(arena, offs, lens, recs) reader getters as SoA device columns
+  zp.stats.count(recs)                       per-protocol / per-error counters (device)
   zp.ring.Ring(device, slots, slot_bytes)    host-ring ingestion (H2D/parse/D2H in flight)
   zp.builder.Chain / BuildBatch              batched PacketBuilder chains on the GPU
   zp.PacketParser.parse(frame)               one frame through the GPU path
@@ -18,8 +19,8 @@ from .parser import (ArpReader, AuthenticationHeaderReader, EthernetReader,  # n
                      RoutingHeaderReader, TcpReader, UdpReader, ZeroPacketError)
 
 try:  # torch-dependent batch API
-    from . import batch, builder, columns  # noqa: F401
+    from . import batch, builder, columns, stats  # noqa: F401
 except ImportError:  # pragma: no cover
-    batch = builder = columns = None
+    batch = builder = columns = stats = None
 
 __all__ = ["PacketParser", "ZeroPacketError", "batch", "records"]

@@ -1,0 +1,136 @@
+// zp_stats.hip — per-batch counters over parse records (SURVEY.md §8(e):
+// "optional aggregate counters (per-protocol counts, error histogram) are
+// summed on the host from 8 small arrays").
+//
+// zp_stats_device adds, for n records, the number of frames with each
+// presence bit set (the nine PacketParser Options of parser.rs:22-32, the
+// IpInIp tag, both Option<ExtensionHeaders> and their slots) and the number
+// of frames per zp_err code (0 = Ok; the reference's Err strings otherwise)
+// into a device array of ZP_STATS_COUNT u64. A multi-GPU job sums its ranks'
+// arrays on the host: the frames are independent, there is no exchange step.
+//
+// HBM-bound on the 16-B records: one dwordx4 load per frame, lane-parallel
+// (SWAR) flag counts, one set of u64 atomics per workgroup.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include "../../include/zero_packet.h"
+
+extern "C" char* zp__errbuf(void);
+
+#define ST_BLOCK 256
+#define ST_WAVES (ST_BLOCK / 64)
+#define ST_U 4                     // records per lane in flight
+#define ST_GLOBAL __attribute__((address_space(1)))
+typedef unsigned st_u32x4 __attribute__((ext_vector_type(4)));
+
+// Lane-parallel counting: bit b of a record's flags is counted in byte b / 8
+// of acc[b % 8] (SWAR, four counters per register), so a record costs eight
+// shift/and/add triples instead of 24 ballots. The bytes are flushed into
+// 32-bit lane counters before they can overflow, and the lanes are summed
+// once at the end. Errors: a ballot for Ok, and one per distinct nonzero
+// code of a wave (rare).
+__global__ void __launch_bounds__(ST_BLOCK)
+zp_stats_kernel(const zp_record* __restrict__ recs, uint64_t n,
+                unsigned long long* __restrict__ counts) {
+    __shared__ uint32_t part[ST_WAVES][ZP_STATS_COUNT];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint32_t fc[ZP_STATS_FLAG_BITS];          // per-lane flag counts
+    uint32_t ec[ZP_ERR_COUNT];                // wave-uniform error counts
+#pragma unroll
+    for (int k = 0; k < ZP_STATS_FLAG_BITS; ++k) fc[k] = 0;
+#pragma unroll
+    for (int k = 0; k < ZP_ERR_COUNT; ++k) ec[k] = 0;
+    uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t pending = 0;                     // records in acc (< 256 per byte)
+    const uint64_t stride = (uint64_t)gridDim.x * ST_BLOCK;
+    for (uint64_t i0 = (uint64_t)blockIdx.x * ST_BLOCK + threadIdx.x; i0 - lane < n;
+         i0 += ST_U * stride) {
+        // ST_U records per lane in flight per trip (coalesced 1 KiB wave loads)
+        st_u32x4 q[ST_U];
+#pragma unroll
+        for (int u = 0; u < ST_U; ++u) {
+            const uint64_t i = i0 + u * stride;
+            q[u] = __builtin_nontemporal_load(
+                (const ST_GLOBAL st_u32x4*)(recs + (i < n ? i : n - 1)));
+        }
+#pragma unroll
+        for (int u = 0; u < ST_U; ++u) {
+            const uint64_t i = i0 + u * stride;
+            const bool live = i < n;
+            const uint32_t flags = live ? q[u].x : 0u;
+            const uint32_t err = q[u].y & 0xFFu;    // zp_record: flags, then err at byte 4
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[j] += (flags >> j) & 0x01010101u;
+            const uint64_t ok = __ballot(live && err == 0);
+            ec[0] += (uint32_t)__builtin_popcountll(ok);
+            uint64_t m = __ballot(live) & ~ok;
+            while (m) {                               // wave-uniform, rare
+                const uint32_t e = (uint32_t)__builtin_amdgcn_readlane(
+                    (int)err, (int)__builtin_ctzll(m));
+                const uint64_t hit = __ballot(live && err == e);
+#pragma unroll
+                for (int k = 1; k < ZP_ERR_COUNT; ++k)
+                    if ((uint32_t)k == e) ec[k] += (uint32_t)__builtin_popcountll(hit);
+                m &= ~hit;
+            }
+        }
+        pending += ST_U;
+        if (pending > 255 - ST_U) {                   // uniform: flush the byte counters
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+#pragma unroll
+                for (int y = 0; y < 3; ++y) fc[8 * y + j] += (acc[j] >> (8 * y)) & 0xFFu;
+                acc[j] = 0;
+            }
+            pending = 0;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+#pragma unroll
+        for (int y = 0; y < 3; ++y) fc[8 * y + j] += (acc[j] >> (8 * y)) & 0xFFu;
+    }
+    // lane sums (the flags bits 24-31 are unused: ZP_STATS_FLAG_BITS = 24)
+#pragma unroll
+    for (int k = 0; k < ZP_STATS_FLAG_BITS; ++k) {
+        uint32_t v = fc[k];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+        fc[k] = v;
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < ZP_STATS_FLAG_BITS; ++k) part[wid][ZP_STAT_FLAG(k)] = fc[k];
+#pragma unroll
+        for (int k = 0; k < ZP_ERR_COUNT; ++k) part[wid][ZP_STAT_ERR(k)] = ec[k];
+    }
+    __syncthreads();
+    if (threadIdx.x < ZP_STATS_COUNT) {
+        unsigned long long s = 0;
+        for (int w = 0; w < ST_WAVES; ++w) s += part[w][threadIdx.x];
+        if (s) atomicAdd(&counts[threadIdx.x], s);
+    }
+}
+
+extern "C" int zp_stats_device(const zp_record* records, uint64_t n, uint64_t* counts,
+                               void* stream) {
+    if (n == 0) return 0;
+    if (!records || !counts) {
+        snprintf(zp__errbuf(), 256, "zp_stats_device: null pointer");
+        return -1;
+    }
+    // enough workgroups to fill the chip; each loops over its share
+    uint64_t blocks = (n + ST_BLOCK - 1) / ST_BLOCK;
+    if (blocks > 2048) blocks = 2048;
+    hipLaunchKernelGGL(zp_stats_kernel, dim3((unsigned)blocks), dim3(ST_BLOCK), 0,
+                       (hipStream_t)stream, records, n, (unsigned long long*)counts);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        snprintf(zp__errbuf(), 256, "zp_stats_kernel launch: %s", hipGetErrorString(e));
+        return -2;
+    }
+    return 0;
+}
