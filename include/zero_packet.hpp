@@ -446,6 +446,12 @@ inline void parse_batch_device(const uint8_t* arena, const uint64_t* offs, const
 }
 
 
+// Per-batch counters (zp_stats_device): adds into counts[ZP_STATS_COUNT].
+inline void stats_device(const zp_record* records, uint64_t n, uint64_t* counts, void* stream) {
+    if (zp_stats_device(records, n, counts, stream) < 0)
+        throw std::runtime_error(std::string("zp_stats_device: ") + zp_last_error());
+}
+
 // ---------------------------------------------------------------------------
 // Host-ring ingestion: RAII over zp_ring_*.
 // ---------------------------------------------------------------------------
