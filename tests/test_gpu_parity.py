@@ -176,11 +176,13 @@ def test_edge_lengths_and_empty(zp):
     assert_same(got, gext, want, wext)
 
 
-def _jumbo_ipv6(total_len, rng, valid=True, proto=17):
+def _jumbo_ipv6(total_len, rng, valid=True, proto=17, fill=None):
     """IPv6 UDP/ICMPv6 frame of total_len bytes (payload_length is never
-    checked by the parser, so frames > 64 KiB are legal input)."""
+    checked by the parser, so frames > 64 KiB are legal input); fill: a
+    constant byte instead of random bytes."""
     from pybuilder import internet_checksum, pseudo_header
-    f = bytearray(rng.integers(0, 256, total_len, dtype=np.uint8).tobytes())
+    f = bytearray(rng.integers(0, 256, total_len, dtype=np.uint8).tobytes() if fill is None
+                  else bytes([fill]) * total_len)
     f[12:14] = b"\x86\xdd"
     f[14] = 0x60
     f[20] = proto
@@ -212,6 +214,22 @@ def test_jumbo_frames_exact_path(zp):
     assert_same(got, gext, want, wext)
     # UDP length field wraps for > 64 KiB segments -> UDP_LENGTH; ICMPv6 hits the checksum
     assert set(np.unique(want["err"])) >= {0, ERR["IPV6_L4_CHECKSUM"]}
+
+
+def test_word_sum_bounds(zp):
+    """The largest frames of the stream path (65,536 B) and the first of the
+    exact path (65,537 B), all-0xFF payloads (the largest word sums the u32
+    stream arithmetic meets), valid and corrupt ICMPv6 checksums, at both
+    arena parities."""
+    rng = np.random.default_rng(9)
+    frames = [_jumbo_ipv6(L, rng, ok, 58, fill=0xFF)
+              for L in (65534, 65535, 65536, 65537) for ok in (True, False)]
+    arena, offs, lens = pack(frames)
+    want, wext = orc.parse_batch(arena, offs, lens)
+    assert list(want["err"][0::2]) == [0, 0, 0, 0]
+    for shift in (0, 1):
+        got, gext = gpu_parse(zp, arena, offs, lens, base_shift=shift)
+        assert_same(got, gext, want, wext)
 
 
 def test_all_zero_icmp_never_valid(zp):
