@@ -158,7 +158,7 @@ def main():
                 med = float(np.median(ms))
                 wbytes = n * sum(zp.columns.width(c) for c in names)
                 # records + descriptors + one staged 128-B header window per frame
-                rbytes = n * (32 + 12 + 128)
+                rbytes = n * (16 + 12 + 128)
                 print(f"{cfg} columns[{label}]: {med:8.3f} ms  write {wbytes / med / 1e6:6.0f} GB/s"
                       f"  (write+read {(wbytes + rbytes) / med / 1e6:6.0f} GB/s)  "
                       f"{n / med / 1e3:8.0f} Mpkt/s", flush=True)
