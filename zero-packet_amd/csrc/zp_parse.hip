@@ -55,6 +55,9 @@
 #ifndef ZP_K
 #define ZP_K 1               // consecutive tiles per wave
 #endif
+#ifndef ZP_SMALL_G
+#define ZP_SMALL_G 4         // tiles of at most this many stream items take one small group (0: off)
+#endif
 // Timing-only ablations and diagnostics (tools/build_variants.sh,
 // tools/alloc_probe.py --no-check); never set in the product:
 //   ZP_ABL_FAKE_WALK  replace the walk by "pending L4 at offset 42"
@@ -698,6 +701,18 @@ __device__ __forceinline__ void parse_tiles(const uint8_t* __restrict__ arena,
         STAMP(1);
         // stream: one group of ZP_G items per iteration (group 0 outside the
         // loop, so no load is in flight across the loop back-edge)
+#if ZP_SMALL_G
+        if (s.nitems <= ZP_SMALL_G) {              // wave-uniform: a tile of small frames
+            // One group of ZP_SMALL_G items holds the whole tile (c2: 4 KiB):
+            // no dummy loads past the tile's end (c2 -8 %, c5 -1 %, c3/c4 0).
+            uint4 vs[ZP_SMALL_G];
+            uint32_t ks[ZP_SMALL_G];
+            issue_group<ZP_SMALL_G>(0, s.nitems, s.cur, s.R, lane, fallback, vs, ks);
+            STAMP(2);
+            consume_group<ZP_SMALL_G>(0, s.nitems, lane, vs, ks, win, tail, lds.cend, s.run);
+        } else
+#endif
+        {
         uint4 va[ZP_G];
         uint32_t ka[ZP_G];
         issue_group<ZP_G>(0, s.nitems, s.cur, s.R, lane, fallback, va, ka);
@@ -706,6 +721,7 @@ __device__ __forceinline__ void parse_tiles(const uint8_t* __restrict__ arena,
         for (uint32_t i0 = ZP_G; i0 < s.nitems; i0 += ZP_G) {
             issue_group<ZP_G>(i0, s.nitems, s.cur, s.R, lane, fallback, va, ka);
             consume_group<ZP_G>(i0, s.nitems, lane, va, ka, win, tail, lds.cend, s.run);
+        }
         }
         wave_lds_fence();                          // LDS written by other lanes
 #ifndef ZP_NO_PRIO
