@@ -445,3 +445,30 @@ def test_ext_null_and_sparse(zp):
     e = ext.cpu().numpy()
     untouched = [i for i in range(128) if i != 70]
     assert (e[0, untouched] == 0xA5).all() and (e[1] == 0xA5).all()
+
+
+@pytest.mark.parametrize("cfg", ["c1", "c3"])
+def test_common_frame_path_mutations(zp, cfg):
+    """The straight-line path for Ethernet / IPv4 (20-B header) / TCP, UDP,
+    ICMPv4 frames runs when most of a wave has that shape: mutate header and
+    payload bytes of a quarter of such frames (every check of the path fails
+    somewhere, the rest stay valid) and compare every record with the oracle."""
+    arena, offs, lens = zp.batch.generate(cfg, 40000, first=4242, device=dev())
+    a = arena.cpu().numpy().copy()
+    o, l_ = offs.cpu().numpy(), lens.cpu().numpy()
+    rng = np.random.default_rng(11)
+    pick = rng.random(len(o)) < 0.25
+    for i in np.nonzero(pick)[0]:
+        k = int(rng.integers(0, 4))
+        if k == 0:                              # a header byte (Ethernet, IPv4, L4 words)
+            j = int(rng.choice([12, 13, 14, 16, 17, 22, 23, 24, 25, 34, 35, 38, 39, 46, 47]))
+        elif k == 1:                            # any byte of the first 64
+            j = int(rng.integers(0, 64))
+        else:                                   # any byte (the L4 checksum)
+            j = int(rng.integers(0, int(l_[i])))
+        a[int(o[i]) + j] ^= np.uint8(1 << int(rng.integers(0, 8)))
+    want, wext = orc.parse_batch(a, o, l_)
+    assert (want["err"] == 0).sum() > 25000 and (want["err"] != 0).sum() > 5000
+    for shift in (0, 3):
+        got, gext = gpu_parse(zp, a, o, l_, base_shift=shift)
+        assert_same(got, gext, want, wext)

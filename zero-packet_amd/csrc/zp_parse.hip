@@ -55,6 +55,9 @@
 #ifndef ZP_K
 #define ZP_K 1               // consecutive tiles per wave
 #endif
+#ifndef ZP_FAST_V4
+#define ZP_FAST_V4 1         // straight-line path for Ethernet/IPv4(IHL 5)/TCP|UDP|ICMPv4 (0: off)
+#endif
 #ifndef ZP_SMALL_G
 #define ZP_SMALL_G 4         // tiles of at most this many stream items take one small group (0: off)
 #endif
@@ -553,6 +556,61 @@ struct ViewReader {
     }
 };
 
+// --------------------------------------------------------------------------
+// The common frame, straight-line: Ethernet II without tags, IPv4 with a
+// 20-B header, TCP / UDP / ICMPv4 (c1-c3, most real traffic). Every field of
+// that shape lies in the first 48 bytes, inside the LDS window, so the reads
+// need no bound checks and the sums no loops. fast_v4 accepts a frame only
+// when the general walk would accept it with exactly these readers (every
+// check of parser.rs:153-287 on this path passes); anything else (other
+// shapes, any failing check) takes the general walk, which then finds the
+// first error in the reference's order.
+// --------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t wb8(const FrameView& f, uint32_t x) {
+    const uint32_t y = x + f.shift;
+    return (win_dw(f, y >> 2) >> ((y & 3) * 8)) & 0xFFu;
+}
+__device__ __forceinline__ uint32_t wbe16(const FrameView& f, uint32_t x) {
+    const uint32_t y = x + f.shift, d = y >> 2;
+    const uint32_t t = __builtin_amdgcn_alignbyte(win_dw(f, d + 1), win_dw(f, d), y & 3);
+    return ((t & 0xFFu) << 8) | ((t >> 8) & 0xFFu);
+}
+// V of window bytes [a, a + 4M): M + 1 dword reads, two masks, no loop.
+template <int M>
+__device__ __forceinline__ uint32_t wsum4(const FrameView& f, uint32_t a) {
+    const uint32_t d0 = a >> 2, sh = 8u * (a & 3u);
+    uint32_t V = sad16(win_dw(f, d0) & (~0u << sh), 0u);
+#pragma unroll
+    for (int k = 1; k < M; ++k) V = sad16(win_dw(f, d0 + k), V);
+    return sad16(win_dw(f, d0 + M) & ~(~0u << sh), V);
+}
+// Probe: the frame looks like the common shape (two window reads).
+__device__ __forceinline__ bool v4_probe(const FrameView& f) {
+    return f.len >= 64 && wbe16(f, 12) == 0x0800 && wb8(f, 14) == 0x45;
+}
+__device__ __forceinline__ bool fast_v4(const FrameView& f, Walk& w) {
+    const uint32_t len = f.len;
+    const uint32_t hv = wsum4<5>(f, 14 + f.shift);                  // ipv4.rs:262-264
+    const uint32_t proto = wb8(f, 23);
+    const bool tcp = proto == 6, udp = proto == 17, ic4 = proto == 1;
+    const uint32_t t = wbe16(f, tcp ? 46u : udp ? 38u : 34u);       // one L4 word
+    bool ok = v4_probe(f) && wbe16(f, 16) == len - 14 &&            // parser.rs:188-212
+              hv != 0 && hv % 65535u == 0 && (tcp || udp || ic4);
+    ok = ok && (tcp ? (t >> 12) >= 5 && (t & 0xFFu) != 0             // parser.rs:237-247
+              : udp ? t == len - 34                                  // parser.rs:258-263
+                    : icmpv4_type_ok(t >> 8) && (t & 0xFFu) <= 15);  // parser.rs:273-283
+    const uint32_t pv = wsum4<2>(f, 26 + f.shift);                  // addresses, checksum.rs:38-63
+    const uint32_t ps = (((uintptr_t)f.g + 26) & 1) ? pv : pv * 256u;
+    w.acc = ic4 ? 0u : ps + proto + (len - 34);                     // parser.rs:316-333
+    w.rec.flags = ZP_F_ETHERNET | ZP_F_IPV4 | (tcp ? ZP_F_TCP : udp ? ZP_F_UDP : ZP_F_ICMPV4);
+    w.rec.eth_len = 14;
+    w.rec.l4_off = 34;
+    w.l4 = 34;
+    w.pending = 1;
+    w.v6 = 0;
+    return ok;
+}
+
 // Header walk + checksum verdict + record store of a streamed tile; with COLS
 // also the column views, from the same LDS window (no second pass).
 template <bool COLS>
@@ -580,8 +638,21 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
     w.l4 = 42; w.acc = 0; w.v6 = 0;
     w.rec.flags = ZP_F_ETHERNET;
 #else
-    if (s.live) walk_frame(fv, w);
-    else w.pending = 0;
+    bool done = false;
+#if ZP_FAST_V4
+    // The common shape straight-line when most of the wave has it
+    // (wave-uniform test); the rest of the frames take the general walk.
+    const bool probe = s.live && v4_probe(fv);
+    if (__builtin_popcountll(__ballot(probe)) >= 32) {
+        if (probe) done = fast_v4(fv, w);
+    }
+#endif
+    if (__ballot(s.live && !done)) {
+        if (s.live && !done) {
+            w.rec = zp_record{};
+            walk_frame(fv, w);
+        }
+    }
 #endif
     if (!s.live) return;
     // The frame's stream sum covers the whole chunks [A & ~15, E16):
@@ -724,6 +795,15 @@ __device__ __forceinline__ void parse_tiles(const uint8_t* __restrict__ arena,
         }
         }
         wave_lds_fence();                          // LDS written by other lanes
+        // The frame address again, from its rank's stream origin (live
+        // through the stream anyway) instead of keeping it there: two VGPRs
+        // less at the stream's register peak. Only frames that own chunks
+        // (>= 64 B) ever use it.
+        {
+            const uint32_t r = s.rank & 63u;
+            const uintptr_t org = ((uintptr_t)bperm(s.R.org_hi, r) << 32) | bperm(s.R.org_lo, r);
+            s.ga = org + 16ull * bperm(s.R.pfx, r) + s.shift;
+        }
 #ifndef ZP_NO_PRIO
         __builtin_amdgcn_s_setprio(0);             // walk at priority 0 ...
 #endif
