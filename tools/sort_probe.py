@@ -51,6 +51,7 @@ def main():
     ap.add_argument("--packets", type=int, default=1 << 25)
     ap.add_argument("--windows", default="256,4096,0")
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--shuffle-tiles", action="store_true")
     args = ap.parse_args()
     zp = importlib.import_module("zero-packet_amd")
     lib = zp._lib.hip()
@@ -77,6 +78,15 @@ def main():
         W = n if w == 0 else w
         win = torch.arange(n, device=dev) // W
         perm = torch.argsort(win * 4096 + key, stable=True)
+        if args.shuffle_tiles and w:
+            # same tiles, random tile order inside each window: the kinds do
+            # not land on the same XCD (workgroup b runs on XCD b % 8) in
+            # every window
+            t = perm[: n // W * W].view(n // W, W // 64, 64)
+            g = torch.Generator(device=dev).manual_seed(7)
+            order = torch.argsort(torch.rand(t.shape[:2], device=dev, generator=g), dim=1)
+            t = torch.gather(t, 1, order[:, :, None].expand_as(t))
+            perm = torch.cat([t.reshape(-1), perm[n // W * W:]])
         a2, o2, l2 = regroup(arena, offs, lens, perm)
         f = run(a2, o2, l2)
         f()
@@ -91,7 +101,7 @@ def main():
         for _ in range(3):
             ms += time_launches(f, args.reps // 2)
         t = float(np.median(ms))
-        print(f"{args.config} sorted in windows of {w or 'all'}: {t:.3f} ms "
+        print(f"{args.config} sorted in windows of {w or 'all'}{' (tiles shuffled)' if args.shuffle_tiles else ''}: {t:.3f} ms "
               f"(generator order {base2:.3f} ms, {100 * (t / base2 - 1):+.1f} %)  "
               f"flags/err match: {same}", flush=True)
         del a2, o2, l2, perm
