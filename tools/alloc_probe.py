@@ -45,6 +45,8 @@ def main():
     ap.add_argument("--variants", default="", help="comma list of tools/variants/libzp_<name>.so")
     ap.add_argument("--no-check", action="store_true", help="time variants whose records differ (ablations)")
     ap.add_argument("--parse-only", action="store_true", help="no membw kernels (PMC runs)")
+    ap.add_argument("--colocate", action="store_true",
+                    help="arena and records in one allocation (several gaps and placements)")
     ap.add_argument("--move-records", action="store_true",
                     help="keep the arena, move the records buffer (and variants) instead")
     a = ap.parse_args()
@@ -107,6 +109,34 @@ def main():
                                                        rout.data_ptr(), reg, 0, None))
         print(json.dumps({name: r}), flush=True)
 
+    if a.colocate:
+        # arena and records in ONE allocation: records right after the arena
+        # (2 MiB aligned, plus a gap), or right before it
+        rb = n * 16
+        al = 2 << 20
+        for k in range(a.copies):
+            for gap, before in ((0, False), (64 << 10, False), (al, False), (0, True)):
+                body = (nb + al - 1) // al * al
+                blk = torch.empty(body + gap + rb + al, dtype=torch.uint8, device=dev)
+                if before:
+                    rec2 = blk[:rb].view(n, 16)
+                    a0 = (rb + gap + al - 1) // al * al
+                    ar2 = blk[a0:a0 + nb]
+                else:
+                    ar2 = blk[:nb]
+                    rec2 = blk[body + gap:body + gap + rb].view(n, 16)
+                ar2.copy_(arena)
+                r = timeit(ar2, offs, lens, rec2, inner, a.steps)
+                sep = timeit(ar2, offs, lens, records, inner, a.steps)
+                r["separate_records_med"] = sep["med"]
+                r["arena_ptr"] = hex(ar2.data_ptr())
+                r["rec_ptr"] = hex(rec2.data_ptr())
+                print(json.dumps({f"copy{k} gap={gap >> 10}KiB "
+                                  f"{'before' if before else 'after'}": r}), flush=True)
+                del blk, ar2, rec2
+            hold = torch.empty((k + 1) * (193 << 20), dtype=torch.uint8, device=dev)
+            torch.cuda.empty_cache()
+        return
     if a.move_records:
         hold = []
         for k in range(a.copies):
