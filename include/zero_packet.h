@@ -448,7 +448,11 @@ const char* zp_build_err_str(int code);
  * arena[offs[i] .. offs[i] + lens[i]) (the reference's `&mut [u8]`), its
  * chain is ops[op_start[i] .. op_start[i + 1]) (op_start has n + 1 entries),
  * variable bytes come from `data`. results may be NULL. All pointers are
- * device memory; enqueues on `stream`. Returns 0 or negative on failure. */
+ * device memory; enqueues on `stream`. Returns 0 or negative on failure.
+ * Precondition (not checked on the device, as for zp_parse_batch_device):
+ * every frame lies inside the arena, the frames do not overlap (the kernel
+ * writes them), every op's data range lies inside `data`. The Python API
+ * (BuildBatch.run) checks the descriptors first. */
 int zp_build_batch_device(uint8_t* arena, const uint64_t* offs, const uint32_t* lens,
                           uint64_t n, const zp_build_op* ops, const uint32_t* op_start,
                           const uint8_t* data, zp_build_result* results, void* stream);

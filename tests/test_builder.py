@@ -422,3 +422,28 @@ def test_gpu_builder_lane_path_edges(zp):
     torch.cuda.synchronize()
     assert ta.cpu().numpy().tobytes() == want.tobytes()
     assert got.tobytes() == wres.tobytes()
+
+
+@pytest.mark.gpu
+def test_gpu_builder_descriptor_bounds_refused(zp):
+    """The builder writes into the arena: a frame past its end, a negative
+    length or wrong descriptor dtypes are refused before the kernel runs."""
+    import torch
+    d = torch.device("cuda:0")
+    C = zp.builder.Chain
+    chain = C().ethernet([0] * 6, [1] * 6, 0x0806)
+    arena = torch.zeros(100, dtype=torch.uint8, device=d)
+    for offs, lens in (([40], [64]), ([0], [-1]), ([-8], [64])):
+        with pytest.raises(ValueError):
+            zp.builder.BuildBatch().add(chain).run(
+                arena, torch.tensor(offs, dtype=torch.int64, device=d),
+                torch.tensor(lens, dtype=torch.int32, device=d))
+    with pytest.raises(ValueError):
+        zp.builder.BuildBatch().add(chain).run(
+            arena, torch.tensor([0], dtype=torch.int32, device=d),
+            torch.tensor([64], dtype=torch.int32, device=d))
+    assert int(arena.sum().item()) == 0                  # nothing written
+    res = zp.builder.BuildBatch().add(chain).run(
+        arena, torch.tensor([36], dtype=torch.int64, device=d),
+        torch.tensor([64], dtype=torch.int32, device=d))
+    assert int(res[0]["err"]) == 0 and int(arena[36 + 12].item()) == 0x08

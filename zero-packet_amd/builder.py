@@ -22,6 +22,7 @@ import numpy as np
 import torch
 
 from . import _lib
+from .batch import check_batch
 
 OP_DTYPE = np.dtype([("kind", "u1"), ("b", "u1", (7,)), ("h", "<u2", (4,)), ("w", "<u4", (2,)),
                      ("data_off", "<u4"), ("data_len", "<u4"), ("src", "u1", (16,)),
@@ -169,11 +170,12 @@ class BuildBatch:
     def run(self, arena, offs, lens, stream=None):
         """Executes every chain in place on the device tensors; returns the
         results (numpy RESULT_DTYPE [n])."""
-        for t in (arena, offs, lens):
-            if not t.is_cuda:
-                raise RuntimeError("BuildBatch.run needs device tensors (no CPU fallback)")
+        # the kernel writes into [offs[i], offs[i] + lens[i]) of the arena:
+        # dtypes, devices and bounds are checked before it runs (check_batch)
+        check_batch(arena, offs, lens)
         n = offs.numel()
-        assert n == len(self.chains) and lens.numel() == n
+        if n != len(self.chains):
+            raise ValueError(f"{len(self.chains)} chains for {n} frames")
         ops, op_start, data = self.pack()
         d = arena.device
         t_ops = torch.from_numpy(ops.view(np.uint8)).to(d)

@@ -365,6 +365,26 @@ extern "C" int zp_build_batch_host(zp_ctx* c, uint8_t* arena, uint64_t arena_byt
                                    zp_build_result* results) {
     if (!c || (n && (!arena || !offs || !lens || !ops || !op_start))) return -1;
     if (n == 0) return 0;
+    // host-side checks of what the kernel would read out of bounds
+    if (op_start[n] < op_start[0]) {
+        snprintf(g_ctx_error, ERRBUF_LEN, "zp_build_batch_host: op_start not ascending");
+        return -1;
+    }
+    for (uint64_t k = op_start[0]; k < op_start[n]; ++k) {
+        const zp_build_op& o = ops[k];
+        if (o.data_len != ZP_BUILD_NO_DATA && (uint64_t)o.data_off + o.data_len > data_bytes) {
+            snprintf(g_ctx_error, ERRBUF_LEN,
+                     "zp_build_batch_host: op %llu data range past data_bytes",
+                     (unsigned long long)k);
+            return -1;
+        }
+    }
+    for (uint64_t k = 0; k < n; ++k) {
+        if (op_start[k + 1] < op_start[k]) {
+            snprintf(g_ctx_error, ERRBUF_LEN, "zp_build_batch_host: op_start not ascending");
+            return -1;
+        }
+    }
     int prev = 0;
     (void)hipGetDevice(&prev);
     if (hipSetDevice(c->device) != hipSuccess) return -2;
