@@ -149,3 +149,35 @@ extern "C" int membw_region2(const void* p, uint64_t bytes, uint32_t* out, uint6
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+
+typedef unsigned wg_u32x4 __attribute__((ext_vector_type(4)));
+
+// Write granularity probe: 2^lg16 16-B stores per 128-B line, starting at
+// chunk off16 of the line, over `lines` lines (grid-stride, coalesced).
+template <bool NT>
+__global__ void __launch_bounds__(256) write_gran(uint8_t* __restrict__ p, uint64_t lines,
+                                                  int lg16, int off16, uint32_t v) {
+    const uint64_t total = lines << lg16;
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x; t < total; t += stride) {
+        const uint64_t line = t >> lg16;
+        const uint32_t c = (uint32_t)(t & ((1u << lg16) - 1)) + off16;
+        wg_u32x4* q = (wg_u32x4*)(p + line * 128 + c * 16);
+        const wg_u32x4 x = {v, (uint32_t)t, (uint32_t)line, c};
+        if (NT) __builtin_nontemporal_store(x, q);
+        else *q = x;
+    }
+}
+
+extern "C" int membw_write(void* p, uint64_t lines, int lg16, int off16, int nt, int blocks,
+                           void* stream) {
+    if (lg16 < 0 || lg16 > 3 || off16 < 0 || off16 + (1 << lg16) > 8) return -1;
+    hipStream_t s = (hipStream_t)stream;
+    if (nt)
+        hipLaunchKernelGGL(write_gran<true>, dim3(blocks), dim3(256), 0, s, (uint8_t*)p, lines,
+                           lg16, off16, 7u);
+    else
+        hipLaunchKernelGGL(write_gran<false>, dim3(blocks), dim3(256), 0, s, (uint8_t*)p, lines,
+                           lg16, off16, 7u);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
