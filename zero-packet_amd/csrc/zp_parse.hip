@@ -52,6 +52,9 @@
 #ifndef ZP_WAVES
 #define ZP_WAVES 1           // waves per workgroup (independent waves; 1 = finest LDS granularity)
 #endif
+#ifndef ZP_EXT_DENSE
+#define ZP_EXT_DENSE 32      // chains per wave from which all 64 ext entries are written
+#endif
 #ifndef ZP_K
 #define ZP_K 1               // consecutive tiles per wave
 #endif
@@ -696,13 +699,16 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
         __builtin_nontemporal_store(zp_u32x4{q.x, q.y, q.z, q.w}, (zp_u32x4*)(records + p));
     }
     if (ext) {
-        // The extension chains: a wave with many chains writes the entries of
-        // all its frames (whole lines, zero where absent), one with a few
-        // only those of its chains.
+        // The extension chains: a wave with at least ZP_EXT_DENSE chains
+        // writes the entries of all its frames (whole lines, zero where
+        // absent), one with fewer only those of its chains. Measured on tiles
+        // of k chained frames among IPv4 frames (tools/mix_probe.py): only
+        // the flagged entries is faster up to k = 24 (-2.4 %), equal at 32,
+        // slower from 48 (c4, 56 per wave: +3 %).
         const bool ho = rec.flags & ZP_F_EXT, hi = rec.flags & ZP_F_INNER_EXT;
         const uint64_t mo = __ballot(ho), mi = __ballot(hi);
-        if (mo && (ho || __builtin_popcountll(mo) >= 16)) ext[p] = ho ? w.outer : zp_ext_offsets{};
-        if (mi && (hi || __builtin_popcountll(mi) >= 16)) ext[n + p] = hi ? w.inner : zp_ext_offsets{};
+        if (mo && (ho || __builtin_popcountll(mo) >= ZP_EXT_DENSE)) ext[p] = ho ? w.outer : zp_ext_offsets{};
+        if (mi && (hi || __builtin_popcountll(mi) >= ZP_EXT_DENSE)) ext[n + p] = hi ? w.inner : zp_ext_offsets{};
     }
     if (COLS) {
         ViewReader rdr{fv};
