@@ -787,17 +787,33 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
     uint32_t hl = 0, done = 0, hw = 0;
     const int err = run_chain<ZB_M_WIN>(v, (const uint8_t ZB_LDSP*)nullptr, s.shift, og, nops, wc,
                                         data, lane, &hl, &done, &hw);
-    // write back frame bytes [0, hw) from the region: whole 16-B chunks as
-    // one store, edge chunks byte by byte (never a neighbour's byte)
+    // Write-back of frame bytes [0, hw) from the region: whole 16-B chunks as
+    // one store, edge chunks byte by byte (never a neighbour's byte). A store
+    // that covers part of a 64-B HBM sector costs ~2.4 x a whole one
+    // (read-modify-write), so the header's last sector is
+    // written to its end with the frame's unchanged bytes when the window
+    // holds them (build bench -9 %). Completing the frame's first sector too
+    // would need the previous frame's tail, which the lane does not hold:
+    // re-reading it and writing it back from that frame's lane was +12 %.
     const uintptr_t a0 = s.ga & ~(uintptr_t)15;
-    const uint32_t end = s.shift + (hw < s.wlen ? hw : s.wlen);   // hw <= extent <= wlen
+    const uint32_t sh = s.shift;
+    const uint32_t hwc = hw < s.wlen ? hw : s.wlen;               // hw <= extent <= wlen
+    uint32_t end = sh + hwc;                                      // window coordinates
+#ifndef ZB_NO_SECTOR_WB
+    {
+        const uint32_t se = (uint32_t)(((s.ga + hwc + 63) & ~(uintptr_t)63) - a0);
+        const uint32_t fe = sh + len;
+        const uint32_t e1 = se < fe ? se : fe;                    // never past the frame
+        if (hwc && e1 <= sh + s.wlen) end = e1;                   // bytes in the window
+    }
+#endif
     for (uint32_t c = 0; c < ((end + 15) >> 4); ++c) {
         const uint32_t lo = 16 * c, hi = lo + 16;
-        if (lo >= s.shift && hi <= end) {
+        if (lo >= sh && hi <= end) {
             const uint4 q = ld_region(region, lo);
             *(ZP_GLOBAL zp_u32x4*)(a0 + lo) = zp_u32x4{q.x, q.y, q.z, q.w};
         } else {
-            for (uint32_t b = lo < s.shift ? s.shift : lo; b < (hi < end ? hi : end); ++b)
+            for (uint32_t b = lo < sh ? sh : lo; b < (hi < end ? hi : end); ++b)
                 *(ZP_GLOBAL uint8_t*)(a0 + b) = region[b];
         }
     }
