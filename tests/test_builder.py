@@ -319,8 +319,13 @@ def test_oracle_builder_errors(zp):
 # ---- GPU ---------------------------------------------------------------------
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("seed,big", [(1, False), (2, True)])
-def test_gpu_builder_vs_oracle(zp, seed, big):
+@pytest.mark.parametrize("seed,big,gap", [(1, False, 5), (2, True, 5), (3, False, 0),
+                                          (4, True, 0)])
+def test_gpu_builder_vs_oracle(zp, seed, big, gap):
+    """gap 0 packs the frames back to back: the lane path then also writes the
+    previous frame's unchanged tail bytes of each header's first 64-B sector
+    (when that frame's lane writes nothing there), next to pending, failing
+    and truncated neighbours."""
     import torch
     rng = random.Random(seed)
     chains, lens, fills = [], [], []
@@ -337,7 +342,7 @@ def test_gpu_builder_vs_oracle(zp, seed, big):
         chains.append(c); lens.append(size)
         fills.append(np.array(rb(rng, size), np.uint8) if rng.random() < 0.5
                      else np.zeros(size, np.uint8))
-    before, want, offs, lens_, wres, _ = run_oracle(zp, chains, lens, fill=fills, align=7, gap=5)
+    before, want, offs, lens_, wres, _ = run_oracle(zp, chains, lens, fill=fills, align=7, gap=gap)
     d = torch.device("cuda:0")
     arena = torch.from_numpy(before).to(d)
     batch = zp.builder.BuildBatch()

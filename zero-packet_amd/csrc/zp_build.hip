@@ -728,6 +728,15 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
                      const zp_build_op* __restrict__ ops, const uint32_t* __restrict__ op_start,
                      const uint8_t* __restrict__ data, zp_build_result* __restrict__ results) {
     __shared__ WaveLds lds;
+#ifndef ZB_NO_SECTOR_WB
+    // the 3 chunks before each frame's last one (the previous frame's bytes
+    // in a frame's first 64-B sector)
+    __shared__ uint4 t4[64 * 3];
+    constexpr bool T4 = true;
+#else
+    uint4* t4 = nullptr;
+    constexpr bool T4 = false;
+#endif
     const int lane = threadIdx.x & 63;
     const uint64_t t = blockIdx.x;
     if (t * 64 >= n) return;
@@ -741,75 +750,110 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
     tile_setup(s, t, len, ga, n, lane, lds);
     uint4 va[ZP_G];
     uint32_t ka[ZP_G];
-    issue_group<ZP_G>(0, s.nitems, s.cur, s.R, lane, fallback, va, ka);
-    consume_group<ZP_G>(0, s.nitems, lane, va, ka, win, tail, lds.cend, s.run);
+    issue_group<ZP_G, T4>(0, s.nitems, s.cur, s.R, lane, fallback, va, ka);
+    consume_group<ZP_G, T4>(0, s.nitems, lane, va, ka, win, tail, lds.cend, s.run, t4);
     for (uint32_t i0 = ZP_G; i0 < s.nitems; i0 += ZP_G) {
-        issue_group<ZP_G>(i0, s.nitems, s.cur, s.R, lane, fallback, va, ka);
-        consume_group<ZP_G>(i0, s.nitems, lane, va, ka, win, tail, lds.cend, s.run);
+        issue_group<ZP_G, T4>(i0, s.nitems, s.cur, s.R, lane, fallback, va, ka);
+        consume_group<ZP_G, T4>(i0, s.nitems, lane, va, ka, win, tail, lds.cend, s.run, t4);
     }
     wave_lds_fence();                                  // windows written by other lanes
-    if (!s.live) return;
+    // Every lane stays to the neighbour exchange after the chains; frames
+    // that are not built here are marked pending for the lane-group pass.
     const uint64_t i = t * 64 + lane;
-    const uint32_t o0 = op_start[i], o1 = op_start[i + 1];
-    const uint32_t nops = o1 >= o0 ? o1 - o0 : 0u;
-    const OpGlobal og{ops + o0};
-    const bool fast = o1 >= o0 && len >= 64 && !s.giant && chain_extent(og, nops) <= s.wlen;
-    if (!fast) {
-        zp_build_result r;
-        r.header_len = 0; r.err = (uint8_t)ZB_PENDING; r.ops_done = 0; r.reserved = 0;
-        results[i] = r;
-        return;
+    uint32_t o0 = 0, nops = 0;
+    bool fast = false;
+    if (s.live) {
+        o0 = op_start[i];
+        const uint32_t o1 = op_start[i + 1];
+        nops = o1 >= o0 ? o1 - o0 : 0u;
+        fast = o1 >= o0 && len >= 64 && !s.giant && chain_extent(OpGlobal{ops + o0}, nops) <= s.wlen;
+        if (!fast) {
+            zp_build_result r;
+            r.header_len = 0; r.err = (uint8_t)ZB_PENDING; r.ops_done = 0; r.reserved = 0;
+            results[i] = r;
+        }
     }
+    const OpGlobal og{ops + o0};
     const uint32_t rank = s.rank & 63u;
     const uint32_t nch = (len + s.shift + 15) >> 4;
     WinCsum wc;
-    wc.ga = s.ga;
-    wc.shift = s.shift;
-    wc.len = len;
-    wc.nchw = nch < ZP_WIN_CH ? nch : ZP_WIN_CH;
-    wc.fsum = lds.cend[s.rank] - (s.rank ? lds.cend[s.rank - 1] : 0u);
-    wc.tail = tail[rank];
     uint4 cells[ZP_WIN_CH];
+    uint4 ptail = make_uint4(0, 0, 0, 0);              // the previous frame's last chunk
+    if (fast) {
+        wc.ga = s.ga;
+        wc.shift = s.shift;
+        wc.len = len;
+        wc.nchw = nch < ZP_WIN_CH ? nch : ZP_WIN_CH;
+        wc.fsum = lds.cend[s.rank] - (s.rank ? lds.cend[s.rank - 1] : 0u);
+        wc.tail = tail[rank];
+        ptail = tail[(rank - 1) & 63u];
 #pragma unroll
-    for (uint32_t c = 0; c < ZP_WIN_CH; ++c) {
-        cells[c] = c < wc.nchw ? win[c * 64 + ((rank ^ c) & 63u)] : make_uint4(0, 0, 0, 0);
-        wc.vorig[c] = sad4(cells[c]);
+        for (uint32_t c = 0; c < ZP_WIN_CH; ++c) {
+            cells[c] = c < wc.nchw ? win[c * 64 + ((rank ^ c) & 63u)] : make_uint4(0, 0, 0, 0);
+            wc.vorig[c] = sad4(cells[c]);
+        }
     }
     wave_lds_fence();                                  // every lane holds its cells
     uint8_t ZB_LDSP* region = (uint8_t ZB_LDSP*)win + lane * ZB_RSTRIDE;
-#pragma unroll
-    for (uint32_t c = 0; c < ZP_WIN_CH; ++c) {
-        uint32_t ZB_LDSP* d = (uint32_t ZB_LDSP*)(region + 16 * c);
-        d[0] = cells[c].x; d[1] = cells[c].y; d[2] = cells[c].z; d[3] = cells[c].w;
-    }
-    wc.region = region;
-    BView<uint8_t ZB_LDSP*> v{region + s.shift, len, true};
     uint32_t hl = 0, done = 0, hw = 0;
-    const int err = run_chain<ZB_M_WIN>(v, (const uint8_t ZB_LDSP*)nullptr, s.shift, og, nops, wc,
-                                        data, lane, &hl, &done, &hw);
+    int err = 0;
+    if (fast) {
+#pragma unroll
+        for (uint32_t c = 0; c < ZP_WIN_CH; ++c) {
+            uint32_t ZB_LDSP* d = (uint32_t ZB_LDSP*)(region + 16 * c);
+            d[0] = cells[c].x; d[1] = cells[c].y; d[2] = cells[c].z; d[3] = cells[c].w;
+        }
+        wc.region = region;
+        BView<uint8_t ZB_LDSP*> v{region + s.shift, len, true};
+        err = run_chain<ZB_M_WIN>(v, (const uint8_t ZB_LDSP*)nullptr, s.shift, og, nops, wc,
+                                  data, lane, &hl, &done, &hw);
+    }
     // Write-back of frame bytes [0, hw) from the region: whole 16-B chunks as
-    // one store, edge chunks byte by byte (never a neighbour's byte). A store
-    // that covers part of a 64-B HBM sector costs ~2.4 x a whole one
-    // (read-modify-write), so the header's last sector is
-    // written to its end with the frame's unchanged bytes when the window
-    // holds them (build bench -9 %). Completing the frame's first sector too
-    // would need the previous frame's tail, which the lane does not hold:
-    // re-reading it and writing it back from that frame's lane was +12 %.
+    // one store, edge chunks byte by byte (never a byte another lane writes).
+    // A store that covers part of a 64-B HBM sector costs ~2.4 x a whole one
+    // (read-modify-write), so the lane completes its header's
+    // sectors where it can: the last one to its end with the frame's
+    // unchanged bytes from the window, and the first one from its start with
+    // the previous frame's unchanged tail (the 3 chunks before its last one,
+    // kept by the stream, and the shared chunk from the window) when that
+    // frame ends exactly here and its lane writes nothing there.
     const uintptr_t a0 = s.ga & ~(uintptr_t)15;
     const uint32_t sh = s.shift;
     const uint32_t hwc = hw < s.wlen ? hw : s.wlen;               // hw <= extent <= wlen
-    uint32_t end = sh + hwc;                                      // window coordinates
+    uint32_t end = fast ? sh + hwc : sh;                          // window coordinates
 #ifndef ZB_NO_SECTOR_WB
-    {
+    if (fast) {
         const uint32_t se = (uint32_t)(((s.ga + hwc + 63) & ~(uintptr_t)63) - a0);
         const uint32_t fe = sh + len;
         const uint32_t e1 = se < fe ? se : fe;                    // never past the frame
         if (hwc && e1 <= sh + s.wlen) end = e1;                   // bytes in the window
     }
+    // the previous lane's frame and where its writes end (all lanes active)
+    const uintptr_t wend = a0 + end;
+    const uint32_t pl = lane ? (uint32_t)lane - 1u : 0u;
+    const uintptr_t pA = ((uintptr_t)bperm((uint32_t)(s.ga >> 32), pl) << 32) |
+                         bperm((uint32_t)s.ga, pl);
+    const uintptr_t pW = ((uintptr_t)bperm((uint32_t)(wend >> 32), pl) << 32) |
+                         bperm((uint32_t)wend, pl);
+    const uint32_t pLen = bperm(s.live ? len : 0u, pl);
+    const uintptr_t S0 = s.ga & ~(uintptr_t)63;
+    const bool pre = fast && lane && hwc && (s.ga & 63u) && pLen >= 64 && pLen <= ZP_GIANT &&
+                     pA + pLen == s.ga &&
+                     S0 >= pA && S0 >= pW;
+    if (pre) {
+        const uintptr_t lastc = (s.ga - 1) & ~(uintptr_t)15;      // the previous frame's last chunk
+        for (uintptr_t X = S0; X < a0; X += 16) {
+            const uint32_t d = (uint32_t)((lastc - X) >> 4);      // 0..3
+            const uint4 q = d == 0 ? ptail : t4[(rank - 1) * 3 + d - 1];
+            *(ZP_GLOBAL zp_u32x4*)X = zp_u32x4{q.x, q.y, q.z, q.w};
+        }
+    }
+#else
+    const bool pre = false;
 #endif
     for (uint32_t c = 0; c < ((end + 15) >> 4); ++c) {
         const uint32_t lo = 16 * c, hi = lo + 16;
-        if (lo >= sh && hi <= end) {
+        if ((lo >= sh || (pre && c == 0)) && hi <= end) {
             const uint4 q = ld_region(region, lo);
             *(ZP_GLOBAL zp_u32x4*)(a0 + lo) = zp_u32x4{q.x, q.y, q.z, q.w};
         } else {
@@ -817,6 +861,7 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
                 *(ZP_GLOBAL uint8_t*)(a0 + b) = region[b];
         }
     }
+    if (!fast) return;
     zp_build_result r;
     r.header_len = hl;
     r.err = (uint8_t)err;

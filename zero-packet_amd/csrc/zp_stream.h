@@ -149,6 +149,8 @@ struct Ranked {          // lane r = frame of rank r
 #define KEEP_IN (1u << 31)     // chunk belongs to a frame (else past the end)
 #define KEEP_WIN (1u << 30)    // chunk index < ZP_WIN_CH: window cell in bits 0-9
 #define KEEP_TAIL (1u << 29)   // frame's last chunk
+#define KEEP_T4 (1u << 28)     // one of the 3 chunks before the frame's last (T4 streams) ...
+#define KEEP_T4D(k) (((k) >> 22) & 3u)   // ... at this distance from the last, minus 1
 #define KEEP_CELL(k) ((k) & 0x3FFu)
 #define KEEP_RANK(k) (((k) >> 16) & 63u)
 
@@ -177,7 +179,7 @@ __device__ __forceinline__ void build_starts(uint32_t w0, const Cursor& c, const
 // Always issues exactly G loads (items past the end re-read the wave's last
 // chunk, or a dummy): a static load count keeps the compiler's s_waitcnt
 // exact.
-template <int G>
+template <int G, bool T4 = false>
 __device__ __forceinline__ void issue_group(uint32_t i0, uint32_t nitems, Cursor& c,
                                             const Ranked& R, int lane, uintptr_t fallback,
                                             uint4 (&v)[G], uint32_t (&keep)[G]) {
@@ -230,6 +232,7 @@ __device__ __forceinline__ void issue_group(uint32_t i0, uint32_t nitems, Cursor
         uint32_t k = (r & 63u) << 16;
         k |= ci < ZP_WIN_CH ? KEEP_WIN | (ci * 64u + ((r ^ ci) & 63u)) : 0u;
         k |= vv == lv ? KEEP_TAIL : 0u;
+        if (T4) k |= lv - vv - 1u < 3u ? KEEP_T4 | ((lv - vv - 1u) << 22) : 0u;
         keep[q] = (i < nitems && vv <= lv) ? k | KEEP_IN : 0u;
         const uint32_t vc = vv < lv ? vv : lv;
         a[q] = nitems ? (((uintptr_t)ohi << 32) | olo) + 16ull * vc : fallback;
@@ -251,11 +254,11 @@ __device__ __forceinline__ void retire_group(const uint4 (&v)[G]) {
     for (int q = 0; q < G; ++q) asm volatile("" ::"v"(v[q].x), "v"(v[q].y), "v"(v[q].z), "v"(v[q].w));
 }
 
-template <int G>
+template <int G, bool T4 = false>
 __device__ __forceinline__ void consume_group(uint32_t i0, uint32_t nitems, int lane,
                                               const uint4 (&v)[G], const uint32_t (&keep)[G],
                                               uint4* win, uint4* tail, uint32_t* cend,
-                                              uint32_t& run) {
+                                              uint32_t& run, uint4* t4 = nullptr) {
     // Items past the end (wave-uniform) are skipped by a branch, not a
     // loop exit: with `break` LLVM stops fully unrolling past G = 8 and the
     // group arrays go to scratch.
@@ -265,6 +268,9 @@ __device__ __forceinline__ void consume_group(uint32_t i0, uint32_t nitems, int 
         if (i >= nitems) continue;                            // wave-uniform
         const uint32_t k = keep[q];
         if (k & KEEP_WIN) win[KEEP_CELL(k)] = v[q];
+        // T4 streams (the builder) also keep the 3 chunks before each
+        // frame's last one: t4[rank * 3 + distance from the last - 1]
+        if (T4 && (k & KEEP_T4)) t4[KEEP_RANK(k) * 3 + KEEP_T4D(k)] = v[q];
         uint32_t part = sad16(v[q].x, 0u);
         part = sad16(v[q].y, part);
         part = sad16(v[q].z, part);
