@@ -472,3 +472,46 @@ def test_common_frame_path_mutations(zp, cfg):
     for shift in (0, 3):
         got, gext = gpu_parse(zp, a, o, l_, base_shift=shift)
         assert_same(got, gext, want, wext)
+
+
+@pytest.mark.parametrize("layout", ["packed", "shuffled"])
+def test_min_size_tiles(zp, layout):
+    """Tiles whose frames are all 64 B take the register path; one frame of
+    another shape, or failing a check, sends its whole tile to the stream
+    path. 64-B frames (c1) with a few single-bit flips (header and L4 bytes:
+    wrong shapes, failed checks and checksums), a ragged last tile, every
+    frame alignment mod 4 (packed at base shifts 0-3, or shuffled offsets
+    with gaps), and an ICMP frame whose L4 bytes are all zero."""
+    arena, offs, lens = zp.batch.generate("c1", 64 * 300 + 17, first=99, device=dev())
+    a = arena.cpu().numpy().copy()
+    o, l_ = offs.cpu().numpy().astype(np.int64), lens.cpu().numpy()
+    assert (l_ == 64).all()
+    rng = np.random.default_rng(5)
+    for i in rng.choice(len(o), 60, replace=False):
+        j = int(rng.integers(0, 64))
+        a[o[i] + j] ^= np.uint8(1 << int(rng.integers(0, 8)))
+    frames = [a[x:x + 64].tobytes() for x in o]
+    want_n = None
+    if layout == "packed":
+        pa, po, pl = pack(frames)
+        want, wext = orc.parse_batch(pa, po, pl)
+        want_n = int((want["err"] != 0).sum())
+        for shift in range(4):
+            got, gext = gpu_parse(zp, pa, po, pl, base_shift=shift)
+            assert_same(got, gext, want, wext)
+    else:
+        order = rng.permutation(len(frames))
+        pos, po = 0, np.zeros(len(frames), np.int64)
+        for k in order:
+            pos += int(rng.integers(0, 20))
+            po[k] = pos
+            pos += 64
+        pa = np.zeros(pos + 64, np.uint8)
+        for k, f in enumerate(frames):
+            pa[po[k]:po[k] + 64] = np.frombuffer(f, np.uint8)
+        pl = np.full(len(frames), 64, np.uint32)
+        want, wext = orc.parse_batch(pa, po.astype(np.uint64), pl)
+        want_n = int((want["err"] != 0).sum())
+        got, gext = gpu_parse(zp, pa, po, pl)
+        assert_same(got, gext, want, wext)
+    assert 10 <= want_n <= 60

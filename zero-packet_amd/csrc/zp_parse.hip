@@ -61,6 +61,9 @@
 #ifndef ZP_FAST_V4
 #define ZP_FAST_V4 1         // straight-line path for Ethernet/IPv4(IHL 5)/TCP|UDP|ICMPv4 (0: off)
 #endif
+#ifndef ZP_TINY
+#define ZP_TINY 1            // register path for tiles of 64-B Ethernet/IPv4/L4 frames (0: off)
+#endif
 #ifndef ZP_SMALL_G
 #define ZP_SMALL_G 4         // tiles of at most this many stream items take one small group (0: off)
 #endif
@@ -614,6 +617,72 @@ __device__ __forceinline__ bool fast_v4(const FrameView& f, Walk& w) {
     return ok;
 }
 
+// --------------------------------------------------------------------------
+// Minimum-size frames in registers. A tile whose live frames are all 64 B
+// (the Ethernet minimum; c1/c2, line-rate small-packet traffic) does not need
+// the packed stream, the LDS window or the walk: each lane loads its own
+// frame (4 dwordx4 + 1 dword from A & ~3: never past the 16-B chunk holding
+// the frame's last byte, as the stream), aligns it to 16 frame dwords, and
+// checks the common shape (Ethernet II / IPv4 with a 20-B header / TCP, UDP,
+// ICMPv4) with both checksums from the registers. Word sums are taken at even
+// FRAME offsets, little-endian: a big-endian word w is 256 * (its LE value)
+// mod 65535, and a sum is zero iff all its words are, so the checks of
+// csum_ok hold with `odd` = false. If any live lane's frame is not of that
+// shape or fails a check, the tile takes the stream path, whose walk finds
+// the reference's first error.
+// --------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t tiny_be16(const uint32_t (&f)[16], uint32_t x) {
+    const uint32_t d = f[x >> 2] >> (8 * (x & 2));                 // x even
+    return ((d & 0xFFu) << 8) | ((d >> 8) & 0xFFu);
+}
+__device__ __forceinline__ bool tiny_tile(uint64_t tile, uint32_t len, uintptr_t ga, uint64_t n,
+                                          int lane, zp_record* __restrict__ records) {
+    const bool live = tile * 64 + lane < n;
+    const uintptr_t base = ga & ~(uintptr_t)3;
+    const uint32_t sh = (uint32_t)(ga & 3);
+    uint32_t w[17];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const zp_u32x4 q = *(const ZP_GLOBAL zp_u32x4*)(live ? base + 16 * k : ga);
+        w[4 * k] = q.x; w[4 * k + 1] = q.y; w[4 * k + 2] = q.z; w[4 * k + 3] = q.w;
+    }
+    w[16] = (live && sh) ? *(const ZP_GLOBAL uint32_t*)(base + 64) : 0u;
+    uint32_t f[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) f[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
+    // parser.rs:153-165, 188-212 (IPv4, IHL 5), then the L4 reader of the
+    // protocol (parser.rs:237-283) and the checksum (parser.rs:316-333)
+    const uint32_t proto = f[5] >> 24;
+    const bool tcp = proto == 6, udp = proto == 17, ic4 = proto == 1;
+    const uint32_t hv = sad16(f[3] >> 16, sad16(f[4], sad16(f[5], sad16(f[6], sad16(f[7],
+                            sad16(f[8] & 0xFFFFu, 0u))))));            // bytes 14..33
+    const uint32_t t = tiny_be16(f, tcp ? 46u : udp ? 38u : 34u);
+    bool ok = tiny_be16(f, 12) == 0x0800 && ((f[3] >> 16) & 0xFFu) == 0x45 &&
+              tiny_be16(f, 16) == 50u && hv != 0 && hv % 65535u == 0 && (tcp || udp || ic4);
+    ok = ok && (tcp ? (t >> 12) >= 5 && (t & 0xFFu) != 0
+              : udp ? t == 30u
+                    : icmpv4_type_ok(t >> 8) && (t & 0xFFu) <= 15);
+    const uint32_t pv = sad16(f[6] >> 16, sad16(f[7], sad16(f[8] & 0xFFFFu, 0u)));  // 26..33
+    const uint32_t ps = (pv % 65535u) * 256u;                          // BE address words
+    const uint32_t acc = ic4 ? 0u : ps + proto + 30u;
+    uint32_t lv = sad16(f[8] >> 16, 0u);                               // L4 bytes 34..63
+#pragma unroll
+    for (int k = 9; k < 16; ++k) lv = sad16(f[k], lv);
+    ok = ok && csum_ok(acc, lv, false);
+    if (__ballot(live && !ok)) return false;                           // wave-uniform
+    if (live) {
+        zp_record rec{};
+        rec.flags = ZP_F_ETHERNET | ZP_F_IPV4 | (tcp ? ZP_F_TCP : udp ? ZP_F_UDP : ZP_F_ICMPV4);
+        rec.eth_len = 14;
+        rec.l4_off = 34;
+        uint4 q;
+        memcpy(&q, &rec, sizeof rec);
+        __builtin_nontemporal_store(zp_u32x4{q.x, q.y, q.z, q.w},
+                                    (zp_u32x4*)(records + tile * 64 + lane));
+    }
+    return true;
+}
+
 // Header walk + checksum verdict + record store of a streamed tile; with COLS
 // also the column views, from the same LDS window (no second pass).
 template <bool COLS>
@@ -773,6 +842,12 @@ __device__ __forceinline__ void parse_tiles(const uint8_t* __restrict__ arena,
         uint32_t len;
         uintptr_t ga;
         load_desc(arena, offs, lens, n, t, lane, len, ga);
+#if ZP_TINY
+        // a tile of 64-B frames: registers only (wave-uniform test)
+        if (!COLS && !__ballot(t * 64 + lane < n && len != 64u) &&
+            tiny_tile(t, len, ga, n, lane, records))
+            continue;
+#endif
         TileState s;
         tile_setup(s, t, len, ga, n, lane, lds);
         STAMP(1);
