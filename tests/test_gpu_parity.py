@@ -515,3 +515,20 @@ def test_min_size_tiles(zp, layout):
         got, gext = gpu_parse(zp, pa, po, pl)
         assert_same(got, gext, want, wext)
     assert 10 <= want_n <= 60
+
+
+def test_min_size_tiles_small_batches(zp):
+    """The register path at batch edges: 1, 5, 64 and 65 frames of 64 B, and a
+    tile whose 64 descriptors all name the same frame."""
+    arena, offs, lens = zp.batch.generate("c1", 65, first=7, device=dev())
+    a, o, l_ = arena.cpu().numpy(), offs.cpu().numpy(), lens.cpu().numpy()
+    for n in (1, 5, 64, 65):
+        want, wext = orc.parse_batch(a, o[:n], l_[:n])
+        for shift in (0, 1):
+            got, gext = gpu_parse(zp, a, o[:n], l_[:n], base_shift=shift)
+            assert_same(got, gext, want, wext)
+    same = np.full(64, o[3], np.uint64)
+    want, wext = orc.parse_batch(a, same, l_[:64])
+    got, gext = gpu_parse(zp, a, same, l_[:64])
+    assert_same(got, gext, want, wext)
+    assert (want["err"] == 0).all()
