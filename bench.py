@@ -40,9 +40,10 @@ WORKLOADS = {
     "c3": "16M IPv4 TCP/UDP/ICMPv4, U[64,1500]B (config 3)",
     "c4": "16M IPv6 + HBH/Routing/Fragment + VLAN/QinQ (config 4)",
     "c5": "IMIX 64/576/1500 7:4:1, IPv4/IPv6, 25% IP-in-IP (config 5 shard)",
+    "c6": "16M mixed: c3/c4/c5 shapes + 1/16 ARP per packet (not a BASELINE config)",
 }
 DEFAULT_PACKETS = {"c1": 1 << 20, "c2": 1 << 20, "c3": 1 << 24, "c4": 1 << 24,
-                   "c5": (1 << 28) // 8}
+                   "c5": (1 << 28) // 8, "c6": 1 << 24}
 
 
 def log(*a):

@@ -466,8 +466,9 @@ int zp_build_batch_host(zp_ctx* ctx, uint8_t* arena, uint64_t arena_bytes,
                         const uint8_t* data, uint64_t data_bytes, zp_build_result* results);
 
 /* ------------------------------------------------------------------------- */
-/* Synthetic batch generator (BASELINE.json configs 1-5), built from the      */
-/* builder's checksum-fill semantics (builder.rs:473-474,515-516,553,592-593).*/
+/* Synthetic batch generator (BASELINE.json configs 1-5, mixed config 6),    */
+/* built from the builder's checksum-fill semantics                          */
+/* (builder.rs:473-474,515-516,553,592-593).                                 */
 /* Deterministic per packet: packet i depends only on (config, seed, i).      */
 /* ------------------------------------------------------------------------- */
 #define ZP_CFG_C1_ETH_IPV4_UDP_64 1  /* == C2 layout, CPU plumbing            */
@@ -475,6 +476,9 @@ int zp_build_batch_host(zp_ctx* ctx, uint8_t* arena, uint64_t arena_bytes,
 #define ZP_CFG_C3_IPV4_MIX        3
 #define ZP_CFG_C4_IPV6_EXT_VLAN   4
 #define ZP_CFG_C5_IMIX_IPINIP     5
+#define ZP_CFG_C6_MIXED           6  /* not a BASELINE config: per packet the shape
+                                        of C3, C4 or C5 (5/16 each) or a 64-B ARP
+                                        frame (1/16), so every tile mixes stacks */
 #define ZP_GEN_SEED_DEFAULT 0x5EED2025ull
 
 /* Frame length of packet `first + i`, i in [0, n), into d_lens (device). */

@@ -97,7 +97,7 @@ def getter_columns(zp, frame, rec, ext):
 def frames_corpus(zp, golden, n_fuzz, seed=99):
     rng = random.Random(seed)
     seeds = [bytes.fromhex(fx["bytes"]) for fx in golden["fixtures"]]
-    for cfg in ("c3", "c4", "c5"):
+    for cfg in ("c3", "c4", "c5", "c6"):
         arena, offs, lens = zp.batch.generate_host(cfg, 60, first=4242)
         seeds += [arena[o:o + l].tobytes() for o, l in zip(offs, lens)]
     frames = list(seeds)
@@ -140,7 +140,7 @@ def test_oracle_columns_vs_getters(zp, golden):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", ["corpus", "c3", "c4", "c5"])
+@pytest.mark.parametrize("case", ["corpus", "c3", "c4", "c5", "c6"])
 def test_gpu_columns_vs_oracle(zp, golden, case):
     import torch
     d = torch.device("cuda:0")

@@ -6,7 +6,8 @@ import pytest
 import oracle as orc
 
 
-@pytest.mark.parametrize("cfg,n", [("c1", 2000), ("c3", 3000), ("c4", 3000), ("c5", 4000)])
+@pytest.mark.parametrize("cfg,n", [("c1", 2000), ("c3", 3000), ("c4", 3000), ("c5", 4000),
+                                   ("c6", 6000)])
 def test_generated_frames_accepted(zp, cfg, n):
     arena, offs, lens = zp.batch.generate_host(cfg, n, first=12345)
     rec, _ = orc.parse_batch(arena, offs, lens)
@@ -30,6 +31,17 @@ def test_generated_frames_accepted(zp, cfg, n):
         assert set(np.unique(lens)) == {64, 576, 1500}
         assert 0.10 < ((f & R.F_IP_IN_IP) != 0).mean() < 0.3
         assert ((f & R.F_IP_IN_IP_V6) != 0).any()
+    if cfg == "c6":
+        # every header stack of c3-c5 plus ARP, mixed inside each 64-frame tile
+        assert 0.03 < ((f & R.F_ARP) != 0).mean() < 0.10
+        for b in (R.F_IPV4, R.F_IPV6, R.F_IP_IN_IP, R.F_EXT, R.F_TCP, R.F_UDP, R.F_ICMPV4,
+                  R.F_ICMPV6):
+            assert ((f & b) != 0).any(), b
+        arp = (f & R.F_ARP) != 0
+        assert (lens[arp] == 64).all() and set(np.unique(rec["eth_len"][arp])) == {14, 18, 22}
+        tiles = f[: len(f) // 64 * 64].reshape(-1, 64)
+        assert ((tiles & R.F_IPV4) != 0).any(1).all() and ((tiles & R.F_IPV6) != 0).any(1).all()
+        assert ((tiles & R.F_ARP) != 0).any(1).mean() > 0.9
 
 
 def test_generator_deterministic_per_packet(zp):

@@ -90,7 +90,7 @@ def test_golden_parse_one(zp, golden):
 # ---- synthetic configs ---------------------------------------------------
 
 @pytest.mark.parametrize("cfg,n", [("c1", 50000), ("c3", 40000), ("c4", 40000),
-                                   ("c5", 60000)])
+                                   ("c5", 60000), ("c6", 60000)])
 def test_synthetic_configs_exact(zp, cfg, n):
     arena, offs, lens = zp.batch.generate(cfg, n, first=99991, device=dev())
     r, e = zp.batch.parse_batch(arena, offs, lens)
@@ -101,7 +101,7 @@ def test_synthetic_configs_exact(zp, cfg, n):
     assert_same(got, gext, want, wext)
 
 
-@pytest.mark.parametrize("cfg", ["c1", "c3", "c4", "c5"])
+@pytest.mark.parametrize("cfg", ["c1", "c3", "c4", "c5", "c6"])
 def test_device_generator_matches_host(zp, cfg):
     n = 3000
     a, o, l_ = zp.batch.generate(cfg, n, first=5, device=dev())
@@ -291,13 +291,15 @@ def test_host_path_multi(zp, golden):
 
 # ---- full-size properties (BASELINE configs 3-5) ----------------------------
 
-@pytest.mark.parametrize("config,n", [("c3", 16 << 20), ("c4", 16 << 20), ("c5", 32 << 20)])
+@pytest.mark.parametrize("config,n", [("c3", 16 << 20), ("c4", 16 << 20), ("c5", 32 << 20),
+                                      ("c6", 16 << 20)])
 def test_full_size_properties(zp, config, n):
     """BASELINE configs 3-5 at full per-GPU size (c3/c4: 16M frames; c5: one
-    GPU's shard of the 256M IMIX = 32M frames): every frame accepted, a
-    random sample byte-exact vs the oracle, idempotent re-parse, and flipping
-    one bit of every frame's last byte turns every record into the L4
-    checksum error of its innermost IP version."""
+    GPU's shard of the 256M IMIX = 32M frames) and the mixed config c6:
+    every frame accepted, a random sample byte-exact vs the oracle, idempotent
+    re-parse, and flipping one bit of every frame's last byte turns every
+    record into the L4 checksum error of its innermost IP version (ARP frames,
+    which carry no checksum, stay accepted and unchanged)."""
     from importlib import import_module
     rec = import_module("zero-packet_amd.records")
     arena, offs, lens = zp.batch.generate(config, n, device=dev())
@@ -318,12 +320,15 @@ def test_full_size_properties(zp, config, n):
     ipip = (flags & rec.F_IP_IN_IP) != 0
     v6 = torch.where(ipip, (flags & rec.F_IP_IN_IP_V6) != 0, (flags & rec.F_IPV6) != 0)
     want_err = torch.where(v6, ERR["IPV6_L4_CHECKSUM"], ERR["IPV4_L4_CHECKSUM"]).to(torch.uint8)
+    arp = (flags & rec.F_ARP) != 0
+    want_err[arp] = 0
     del r2, e2
     last = offs + lens.to(torch.int64) - 1
     arena[last] ^= 1
     r3, _ = zp.batch.parse_batch(arena, offs, lens)
     torch.cuda.synchronize()
     assert torch.equal(r3[:, 4], want_err)
+    assert torch.equal(r3[arp], r1[arp])
 
 
 # ---- maximum size: the whole BASELINE config 5 on one GPU ------------------

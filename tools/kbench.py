@@ -60,7 +60,8 @@ def main():
         print(f"resident blocks (persistent grid): {rb.zp_debug_resident_blocks()}", flush=True)
     except AttributeError:
         pass
-    sizes = {"c1": 1 << 20, "c2": 1 << 20, "c3": 1 << 24, "c4": 1 << 24, "c5": 1 << 25}
+    sizes = {"c1": 1 << 20, "c2": 1 << 20, "c3": 1 << 24, "c4": 1 << 24, "c5": 1 << 25,
+             "c6": 1 << 24}
     if args.membw:
         mb = ctypes.CDLL(os.path.join(ROOT, "tools", "libmembw.so"))
         mb.membw_read.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,

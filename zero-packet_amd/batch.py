@@ -19,7 +19,7 @@ import torch
 from . import _lib
 from .records import EXT_BYTES, EXT_DTYPE, RECORD_BYTES, RECORD_DTYPE
 
-CONFIGS = {"c1": 1, "c2": 2, "c3": 3, "c4": 4, "c5": 5}
+CONFIGS = {"c1": 1, "c2": 2, "c3": 3, "c4": 4, "c5": 5, "c6": 6}
 SEED = 0x5EED2025
 
 

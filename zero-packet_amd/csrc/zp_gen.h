@@ -69,7 +69,7 @@ enum {
     ZP_S_LEN = 1, ZP_S_VLAN, ZP_S_OUTER, ZP_S_INNER, ZP_S_L4, ZP_S_EXT,
     ZP_S_HBH, ZP_S_RT, ZP_S_DOFF, ZP_S_ICMP, ZP_S_MAC, ZP_S_TCI,
     ZP_S_IP4O, ZP_S_IP4I, ZP_S_IP6O, ZP_S_IP6I, ZP_S_L4F, ZP_S_PAY,
-    ZP_S_EXTDATA, ZP_S_FLAGS
+    ZP_S_EXTDATA, ZP_S_FLAGS, ZP_S_MIX, ZP_S_ARP
 };
 
 typedef struct zp_plan {
@@ -82,7 +82,7 @@ typedef struct zp_plan {
     uint16_t l4_hdr;       /* L4 header bytes (TCP doff*4, else 8)           */
     uint16_t pay_off;      /* first payload byte                             */
     uint8_t  vlan;         /* 0 none, 1 802.1Q, 2 Q-in-Q                     */
-    uint8_t  outer;        /* 4 or 6                                         */
+    uint8_t  outer;        /* 4 or 6; 0 = ARP (config 6)                     */
     uint8_t  inner;        /* 0, 4 or 6                                      */
     uint8_t  l4;           /* 6 TCP, 17 UDP, 1 ICMPv4, 58 ICMPv6             */
     uint8_t  ext_mask;     /* outer IPv6: 1 HBH, 2 Routing, 4 Fragment       */
@@ -98,6 +98,11 @@ ZP_HD uint32_t zp_ip_hdr_len(uint8_t v) { return v == 4 ? 20u : (v == 6 ? 40u : 
 ZP_HD uint32_t zp_plan_layout(zp_plan* p) {
     uint32_t pos = p->eth_len;
     uint32_t ext = 0;
+    if (p->outer == 0) {           /* ARP: 28-B header, then padding (arp.rs:121-176) */
+        p->ext_len = 0; p->inner_off = 0; p->l4_hdr = 0;
+        p->l4_off = p->pay_off = (uint16_t)(pos + 28u);
+        return pos + 28u;
+    }
     if (p->outer == 6) {
         if (p->ext_mask & 1) ext += ((uint32_t)p->hbh_el + 1u) * 8u;
         if (p->ext_mask & 2) ext += ((uint32_t)p->rt_el + 1u) * 8u;
@@ -120,6 +125,14 @@ ZP_HD uint32_t zp_imix_len(uint64_t h) {
     return r < 7 ? 64u : (r < 11 ? 576u : 1500u);
 }
 
+/* Config 6 (mixed traffic, no BASELINE counterpart): each packet takes the
+ * shape of config 3, 4 or 5 (5/16 each) or is an ARP request / reply (1/16,
+ * 64 B, any tagging), so every 64-frame tile mixes all header stacks. */
+ZP_HD int zp_mix_shape(uint64_t key) {
+    const uint32_t r = zp_below(zp_h(key, ZP_S_MIX), 16);
+    return r == 0 ? 0 : (r <= 5 ? 3 : (r <= 10 ? 4 : 5));
+}
+
 /* Draws the structure of packet `idx` (everything except checksums). */
 ZP_HD void zp_plan_packet(int cfg, uint64_t seed, uint64_t idx, zp_plan* p) {
     const uint64_t key = zp_mix64(seed ^ (idx * ZP_GOLDEN));
@@ -129,6 +142,17 @@ ZP_HD void zp_plan_packet(int cfg, uint64_t seed, uint64_t idx, zp_plan* p) {
     p->icmp_code = 0; p->csum_o4 = 0; p->csum_i4 = 0; p->csum_l4 = 0;
     p->tcp_flags = (uint8_t)(1u + zp_below(zp_h(key, ZP_S_FLAGS), 255));
     uint32_t len = 64;
+    if (cfg == 6) {
+        cfg = zp_mix_shape(key);
+        if (cfg == 0) {                   /* ARP */
+            p->outer = 0; p->l4 = 0;
+            p->vlan = (uint8_t)zp_below(zp_h(key, ZP_S_VLAN), 3);
+            p->eth_len = (uint16_t)(14u + 4u * p->vlan);
+            zp_plan_layout(p);
+            p->len = 64;
+            return;
+        }
+    }
     if (cfg == 3) {                       /* IPv4, TCP/UDP/ICMPv4, U[64,1500] */
         len = 64u + zp_below(zp_h(key, ZP_S_LEN), 1437);
         uint32_t l4 = zp_below(zp_h(key, ZP_S_L4), 3);
@@ -237,7 +261,7 @@ ZP_HD uint8_t zp_gen_byte(const zp_plan* p, uint32_t pos) {
     const uint64_t key = p->key;
     if (pos < p->eth_len) {
         if (pos < 12) return zp_hbyte(key, ZP_S_MAC, pos);
-        uint32_t ethertype = p->outer == 4 ? 0x0800u : 0x86DDu;
+        uint32_t ethertype = p->outer == 4 ? 0x0800u : (p->outer == 6 ? 0x86DDu : 0x0806u);
         uint32_t w;   /* 16-bit word at [pos & ~1] */
         uint32_t x = pos - 12;
         if (p->vlan == 0) w = ethertype;
@@ -247,6 +271,20 @@ ZP_HD uint8_t zp_gen_byte(const zp_plan* p, uint32_t pos) {
         return (uint8_t)((x & 1) ? w : (w >> 8));
     }
     uint32_t l3 = p->eth_len;
+    if (p->outer == 0) {                   /* ARP (arp.rs:130-227 getters) */
+        if (pos < l3 + 28u) {
+            const uint32_t x = pos - l3;
+            if (x == 0 || x == 3) return 0;                     /* htype 1, ptype 0x0800 */
+            if (x == 1) return 1;
+            if (x == 2) return 8;
+            if (x == 4) return 6;                               /* hlen */
+            if (x == 5) return 4;                               /* plen */
+            if (x == 6) return 0;
+            if (x == 7) return (uint8_t)(1u + zp_below(zp_h(key, ZP_S_ARP), 2));  /* oper 1|2 */
+            return zp_hbyte(key, ZP_S_ARP + 1, x);             /* sha spa tha tpa */
+        }
+        return zp_hbyte(key, ZP_S_PAY, pos - p->pay_off);
+    }
     if (p->outer == 4) {
         if (pos < l3 + 20u)
             return zp_ip4_byte(p, l3, pos - l3, zp_after_ext(p, 0), p->csum_o4, ZP_S_IP4O);
@@ -335,6 +373,7 @@ ZP_HD uint32_t zp_gen_sum(const zp_plan* p, uint32_t lo, uint32_t hi) {
  * (checksum.rs:38-69; ICMPv4 under IPv4 uses no pseudo-header, parser.rs:322). */
 ZP_HD uint32_t zp_gen_pseudo(const zp_plan* p) {
     uint8_t ip = p->inner ? p->inner : p->outer;
+    if (ip == 0) return 0;                      /* ARP: no L4 */
     uint32_t base = p->inner ? p->inner_off : p->eth_len;
     uint32_t seglen = p->len - p->l4_off;
     if (ip == 4) {

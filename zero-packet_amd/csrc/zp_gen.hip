@@ -105,7 +105,7 @@ zp_gen_frames_kernel(int cfg, uint64_t seed, uint64_t first, uint64_t n,
 extern "C" int zp_gen_lengths_device(int config, uint64_t seed, uint64_t first, uint64_t n,
                                      uint32_t* lens, void* stream) {
     if (n == 0) return 0;
-    if (config < 1 || config > 5 || !lens) return -1;
+    if (config < 1 || config > 6 || !lens) return -1;
     uint64_t blocks = (n + 255) / 256;
     hipLaunchKernelGGL(zp_gen_lengths_kernel, dim3((unsigned)blocks), dim3(256), 0,
                        (hipStream_t)stream, config, seed, first, n, lens);
@@ -117,7 +117,7 @@ extern "C" int zp_gen_frames_device(int config, uint64_t seed, uint64_t first, u
                                     const uint32_t* lens, void* stream) {
     (void)lens;
     if (n == 0) return 0;
-    if (config < 1 || config > 5 || !arena || !offs) return -1;
+    if (config < 1 || config > 6 || !arena || !offs) return -1;
     uint64_t waves = n < (1ull << 20) ? n : (1ull << 20);
     uint64_t blocks = (waves + 3) / 4;
     hipLaunchKernelGGL(zp_gen_frames_kernel, dim3((unsigned)blocks), dim3(256), 0,

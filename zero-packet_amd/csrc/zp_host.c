@@ -13,7 +13,7 @@
 
 int zp_host_gen_lengths(int config, uint64_t seed, uint64_t first, uint64_t n,
                         uint32_t* lens) {
-    if (config < 1 || config > 5) return -1;
+    if (config < 1 || config > 6) return -1;
     for (uint64_t i = 0; i < n; ++i) {
         zp_plan p;
         zp_plan_packet(config, seed, first + i, &p);
@@ -51,7 +51,7 @@ static void* worker(void* a) {
 
 int zp_host_gen_frames(int config, uint64_t seed, uint64_t first, uint64_t n,
                        uint8_t* arena, const uint64_t* offs, int nthreads) {
-    if (config < 1 || config > 5) return -1;
+    if (config < 1 || config > 6) return -1;
     if (nthreads <= 0) nthreads = (int)sysconf(_SC_NPROCESSORS_ONLN);
     if (nthreads > 64) nthreads = 64;
     if ((uint64_t)nthreads > n) nthreads = n ? (int)n : 1;
