@@ -126,7 +126,8 @@ def main():
         del copies
         torch.cuda.empty_cache()
     for cfg in [c for c in args.configs.split(",") if c]:
-        n = sizes[cfg]
+        cfg, _, nn = cfg.partition(":")            # "c3:1048576": another batch size
+        n = int(nn) if nn else sizes[cfg]
         arena, offs, lens = zp.batch.generate(cfg, n, device=dev)
         rec = torch.empty((n, 16), dtype=torch.uint8, device=dev)
         ext = torch.empty((2, n, 16), dtype=torch.uint8, device=dev)
