@@ -95,6 +95,10 @@ def getter_columns(zp, frame, rec, ext):
 
 
 def frames_corpus(zp, golden, n_fuzz, seed=99):
+    """Golden and generated frames plus n_fuzz mutations of them; two thirds of
+    the mutations get their checksums refilled (tests/fuzzfix.py), so most are
+    accepted and their columns carry mutated field values."""
+    from fuzzfix import repair
     rng = random.Random(seed)
     seeds = [bytes.fromhex(fx["bytes"]) for fx in golden["fixtures"]]
     for cfg in ("c3", "c4", "c5", "c6"):
@@ -102,7 +106,8 @@ def frames_corpus(zp, golden, n_fuzz, seed=99):
         seeds += [arena[o:o + l].tobytes() for o, l in zip(offs, lens)]
     frames = list(seeds)
     for _ in range(n_fuzz):
-        frames.append(mutate(rng, rng.choice(seeds)))
+        f = mutate(rng, rng.choice(seeds))
+        frames.append(repair(f) if rng.random() < 2 / 3 else f)
     return frames
 
 

@@ -112,10 +112,14 @@ def test_device_generator_matches_host(zp, cfg):
 
 # ---- fuzz & layouts -------------------------------------------------------
 
-def fuzz_frames(zp, golden, count, seed):
+def fuzz_frames(zp, golden, count, seed, repair_p=0.0):
+    """Mutated golden and generated frames; with repair_p, that share of them
+    gets its checksums refilled (tests/fuzzfix.py) so it reaches the checks
+    after the checksums and the accept path."""
+    from fuzzfix import repair
     rng = random.Random(seed)
     seeds = [bytes.fromhex(fx["bytes"]) for fx in golden["fixtures"]]
-    for cfg in ("c3", "c4", "c5"):
+    for cfg in ("c3", "c4", "c5") + (("c1", "c6") if repair_p else ()):
         a, o, l_ = zp.batch.generate_host(cfg, 64, first=seed)
         seeds += [a[x:x + y].tobytes() for x, y in zip(o, l_)]
     out = []
@@ -123,6 +127,8 @@ def fuzz_frames(zp, golden, count, seed):
         f = rng.choice(seeds)
         for _ in range(rng.randint(0, 2)):
             f = mutate(rng, f)
+        if repair_p and rng.random() < repair_p:
+            f = repair(f)
         out.append(f)
     return out
 
@@ -134,6 +140,53 @@ def test_fuzz_gpu_vs_oracle(zp, golden):
     want, wext = orc.parse_batch(arena, offs, lens)
     assert_same(got, gext, want, wext)
     assert len(np.unique(want["err"])) >= 18
+
+
+def test_fuzz_repaired_gpu_vs_oracle(zp, golden):
+    """Mutations with refilled checksums: most frames pass the checksums, so
+    the straight-line IPv4 path, the general walk's field checks and the
+    accept path all see mutated headers."""
+    frames = fuzz_frames(zp, golden, 60000, 11, repair_p=0.7)
+    arena, offs, lens = pack(frames)
+    want, wext = orc.parse_batch(arena, offs, lens)
+    assert (want["err"] == 0).mean() > 0.4
+    for shift in (0, 3):
+        got, gext = gpu_parse(zp, arena, offs, lens, base_shift=shift)
+        assert_same(got, gext, want, wext)
+
+
+def test_min_size_tiles_repaired(zp):
+    """The register path for tiles of 64-B frames against mutated frames that
+    still carry valid checksums: one or two frames per tile get a header or
+    L4 byte changed (bytes 12-63, length kept) and their checksums refilled.
+    A tile is accepted on the register path only if every frame passes its
+    checks; otherwise the whole tile takes the stream path. Both must match
+    the oracle, and both must occur."""
+    from fuzzfix import repair
+    n = 64 * 400
+    arena, offs, lens = zp.batch.generate("c1", n, first=4242, device=dev())
+    a = arena.cpu().numpy().copy()
+    o = offs.cpu().numpy().astype(np.int64)
+    rng = random.Random(17)
+    for t in range(n // 64):
+        for _ in range(rng.randint(1, 2)):
+            i = 64 * t + rng.randrange(64)
+            f = bytearray(a[o[i]:o[i] + 64].tobytes())
+            f[rng.randrange(12, 64)] = rng.choice([0, 1, 2, 4, 5, 6, 15, 16, 17, 0x40, 0x45,
+                                                   0x46, 0x50, 0xF0, 255, rng.randrange(256)])
+            if rng.random() < 0.85:
+                f = repair(bytes(f))
+            a[o[i]:o[i] + 64] = np.frombuffer(bytes(f), np.uint8)
+    lens_np = lens.cpu().numpy()
+    want, wext = orc.parse_batch(a, o.astype(np.uint64), lens_np)
+    ok_tiles = (want["err"].reshape(-1, 64) == 0).all(1).mean()
+    assert 0.2 < ok_tiles < 0.9, ok_tiles
+    for shift in (0, 2):
+        got, gext = gpu_parse(zp, a, o, lens_np, base_shift=shift)
+        assert_same(got, gext, want, wext)
+    # the field checks around the checksums are reached: IPv4 version, total
+    # length, TCP data offset, UDP length
+    assert {9, 12, 26, 29} <= set(np.unique(want["err"]).tolist())
 
 
 @pytest.mark.parametrize("layout", ["shuffled", "gaps", "overlap", "reverse", "dup"])

@@ -50,3 +50,37 @@ def test_fuzz_oracle_vs_pyref(zp, golden):
         errs.add(int(rec["err"]))
     # the fuzz reaches a broad set of error paths
     assert len(errs) >= 18, sorted(errs)
+
+
+def test_fuzz_repaired_oracle_vs_pyref(zp, golden):
+    """Mutations whose checksums are then refilled (tests/fuzzfix.py) get past
+    the checksum checks into the field checks after them and into the accept
+    path: the C oracle and the Python restatement still agree on every
+    record, and the campaign reaches both outcomes broadly."""
+    from fuzzfix import repair
+    rng = random.Random(4321)
+    seeds = [bytes.fromhex(fx["bytes"]) for fx in golden["fixtures"]]
+    for cfg in ("c1", "c3", "c4", "c5", "c6"):
+        arena, offs, lens = zp.batch.generate_host(cfg, 40, first=778)
+        seeds += [arena[o:o + l].tobytes() for o, l in zip(offs, lens)]
+    errs, ok = set(), 0
+    for it in range(4000):
+        frame = mutate(rng, rng.choice(seeds))
+        if rng.random() < 0.3:
+            frame = mutate(rng, frame)
+        if rng.random() < 0.3 and len(frame) > 64:
+            # L4 header fields of the common IPv4 shape (offsets 34-61)
+            f = bytearray(frame)
+            f[rng.randrange(34, 62)] = rng.choice([0, 1, 2, 4, 5, 15, 16, 0x40, 0x50, 0xF0, 255])
+            frame = bytes(f)
+        frame = repair(frame)
+        _, rec, ext = orc.parse_one(frame)
+        got = pyref.to_record_tuple(pyref.parse(frame), ERR)
+        assert rec_tuple(rec, ext) == got, (it, frame.hex())
+        errs.add(int(rec["err"]))
+        ok += int(rec["err"]) == 0
+    assert ok > 1000, ok
+    assert len(errs) >= 15, sorted(errs)
+    # past the checksums: the L4 field checks are reached
+    for e in ("TCP_DATA_OFFSET", "UDP_LENGTH", "ICMPV4_TYPE", "ICMPV4_CODE"):
+        assert ERR[e] in errs, e
