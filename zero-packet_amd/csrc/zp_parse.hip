@@ -705,6 +705,12 @@ __device__ __forceinline__ bool tiny_tile(uint64_t tile, uint32_t len, uintptr_t
     return true;
 }
 
+__device__ __forceinline__ void store_ext(zp_ext_offsets* dst, const zp_ext_offsets& e) {
+    uint4 q;
+    memcpy(&q, &e, sizeof e);
+    __builtin_nontemporal_store(zp_u32x4{q.x, q.y, q.z, q.w}, (zp_u32x4*)dst);
+}
+
 // Header walk + checksum verdict + record store of a streamed tile; with COLS
 // also the column views, from the same LDS window (no second pass).
 template <bool COLS>
@@ -795,11 +801,14 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
         // absent), one with fewer only those of its chains. Measured on tiles
         // of k chained frames among IPv4 frames (tools/mix_probe.py): only
         // the flagged entries is faster up to k = 24 (-2.4 %), equal at 32,
-        // slower from 48 (c4, 56 per wave: +3 %).
+        // slower from 48 (c4, 56 per wave: +3 %). Nontemporal like the
+        // records (c4 -1.3 %, c6 -2.1 %).
         const bool ho = rec.flags & ZP_F_EXT, hi = rec.flags & ZP_F_INNER_EXT;
         const uint64_t mo = __ballot(ho), mi = __ballot(hi);
-        if (mo && (ho || __builtin_popcountll(mo) >= ZP_EXT_DENSE)) ext[p] = ho ? w.outer : zp_ext_offsets{};
-        if (mi && (hi || __builtin_popcountll(mi) >= ZP_EXT_DENSE)) ext[n + p] = hi ? w.inner : zp_ext_offsets{};
+        if (mo && (ho || __builtin_popcountll(mo) >= ZP_EXT_DENSE))
+            store_ext(ext + p, ho ? w.outer : zp_ext_offsets{});
+        if (mi && (hi || __builtin_popcountll(mi) >= ZP_EXT_DENSE))
+            store_ext(ext + n + p, hi ? w.inner : zp_ext_offsets{});
     }
     if (COLS) {
         ViewReader rdr{fv};
