@@ -111,8 +111,10 @@ def main():
         ms = float(np.median([a.elapsed_time(b) for a, b in ev]))
         nbytes = int(ln.sum())
         hdr = n * 54
+        opb = int(t_ops.numel() + t_start.numel() * 4)
         print(f"build c3 x {n} [{name}]: {ms:.3f} ms  {n / ms / 1e3:.0f} Mpkt/s  "
-              f"{(nbytes + hdr) / ms / 1e6:.0f} GB/s (frame read + header write)  errors {errs}",
+              f"{(nbytes + hdr) / ms / 1e6:.0f} GB/s (frame read + header write; "
+              f"{(nbytes + hdr + opb) / ms / 1e6:.0f} with the op reads)  errors {errs}",
               flush=True)
     recs, _ = zp.batch.parse_batch(arena, offs, lens)
     torch.cuda.synchronize()

@@ -637,9 +637,10 @@ __device__ __forceinline__ uint32_t sad4(uint4 q) {
 
 // After the stream each lane copies its window out of the swizzled
 // [chunk][rank] cells into a private contiguous region of the same LDS
-// (ZB_RSTRIDE = 33 dwords per lane: the lanes' accesses to a same offset
-// fall in 64 different banks), so the chain addresses bytes directly.
-#define ZB_RSTRIDE 132
+// (ZB_RSTRIDE = ZP_WIN / 4 + 1 dwords per lane, an odd count: the lanes'
+// accesses to a same offset fall in 64 different banks), so the chain
+// addresses bytes directly.
+#define ZB_RSTRIDE (ZP_WIN + 4)
 static_assert(64 * ZB_RSTRIDE <= (ZP_WIN_CH + 1) * 64 * 16, "regions must fit the window LDS");
 
 __device__ __forceinline__ uint4 ld_region(const uint8_t ZB_LDSP* r, uint32_t at) {
