@@ -22,7 +22,13 @@ extern "C" char* zp__errbuf(void);
 
 #define ST_BLOCK 256
 #define ST_WAVES (ST_BLOCK / 64)
+#ifndef ST_U
 #define ST_U 4                     // records per lane in flight
+#endif
+#ifndef ST_GRID
+#define ST_GRID 512                // workgroups at most: 2 per CU, each looping over its
+#endif                             // share (2048: 63 us per 16M records, 512: 48 us; the
+                                   // per-workgroup atomics contend)
 #define ST_GLOBAL __attribute__((address_space(1)))
 typedef unsigned st_u32x4 __attribute__((ext_vector_type(4)));
 
@@ -30,19 +36,22 @@ typedef unsigned st_u32x4 __attribute__((ext_vector_type(4)));
 // of acc[b % 8] (SWAR, four counters per register), so a record costs eight
 // shift/and/add triples instead of 24 ballots. The bytes are flushed into
 // 32-bit lane counters before they can overflow, and the lanes are summed
-// once at the end. Errors: a ballot for Ok, and one per distinct nonzero
-// code of a wave (rare).
-__global__ void __launch_bounds__(ST_BLOCK)
+// once at the end. Errors: a ballot for Ok (a wave-uniform, scalar count),
+// and one per distinct nonzero code of a wave (rare), counted in the wave's
+// LDS row, so no per-code register is live (64 VGPRs: 8 waves per SIMD, the
+// whole grid resident at once).
+__global__ void __launch_bounds__(ST_BLOCK) __attribute__((amdgpu_waves_per_eu(8)))
 zp_stats_kernel(const zp_record* __restrict__ recs, uint64_t n,
                 unsigned long long* __restrict__ counts) {
     __shared__ uint32_t part[ST_WAVES][ZP_STATS_COUNT];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     uint32_t fc[ZP_STATS_FLAG_BITS];          // per-lane flag counts
-    uint32_t ec[ZP_ERR_COUNT];                // wave-uniform error counts
+    uint32_t* const ec = &part[wid][ZP_STAT_ERR(0)];   // this wave's error counts (LDS)
 #pragma unroll
     for (int k = 0; k < ZP_STATS_FLAG_BITS; ++k) fc[k] = 0;
-#pragma unroll
-    for (int k = 0; k < ZP_ERR_COUNT; ++k) ec[k] = 0;
+    for (int k = lane; k < ZP_ERR_COUNT; k += 64) ec[k] = 0;
+    uint32_t ok_count = 0;                    // wave-uniform
+    __syncthreads();                          // the zeroed rows before any update
     uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t pending = 0;                     // records in acc (< 256 per byte)
     const uint64_t stride = (uint64_t)gridDim.x * ST_BLOCK;
@@ -65,15 +74,13 @@ zp_stats_kernel(const zp_record* __restrict__ recs, uint64_t n,
 #pragma unroll
             for (int j = 0; j < 8; ++j) acc[j] += (flags >> j) & 0x01010101u;
             const uint64_t ok = __ballot(live && err == 0);
-            ec[0] += (uint32_t)__builtin_popcountll(ok);
+            ok_count += (uint32_t)__builtin_popcountll(ok);
             uint64_t m = __ballot(live) & ~ok;
             while (m) {                               // wave-uniform, rare
                 const uint32_t e = (uint32_t)__builtin_amdgcn_readlane(
                     (int)err, (int)__builtin_ctzll(m));
                 const uint64_t hit = __ballot(live && err == e);
-#pragma unroll
-                for (int k = 1; k < ZP_ERR_COUNT; ++k)
-                    if ((uint32_t)k == e) ec[k] += (uint32_t)__builtin_popcountll(hit);
+                if (lane == 0 && e < ZP_ERR_COUNT) ec[e] += (uint32_t)__builtin_popcountll(hit);
                 m &= ~hit;
             }
         }
@@ -104,8 +111,7 @@ zp_stats_kernel(const zp_record* __restrict__ recs, uint64_t n,
     if (lane == 0) {
 #pragma unroll
         for (int k = 0; k < ZP_STATS_FLAG_BITS; ++k) part[wid][ZP_STAT_FLAG(k)] = fc[k];
-#pragma unroll
-        for (int k = 0; k < ZP_ERR_COUNT; ++k) part[wid][ZP_STAT_ERR(k)] = ec[k];
+        ec[0] = ok_count;
     }
     __syncthreads();
     if (threadIdx.x < ZP_STATS_COUNT) {
@@ -124,7 +130,7 @@ extern "C" int zp_stats_device(const zp_record* records, uint64_t n, uint64_t* c
     }
     // enough workgroups to fill the chip; each loops over its share
     uint64_t blocks = (n + ST_BLOCK - 1) / ST_BLOCK;
-    if (blocks > 2048) blocks = 2048;
+    if (blocks > ST_GRID) blocks = ST_GRID;
     hipLaunchKernelGGL(zp_stats_kernel, dim3((unsigned)blocks), dim3(ST_BLOCK), 0,
                        (hipStream_t)stream, records, n, (unsigned long long*)counts);
     const hipError_t e = hipGetLastError();
