@@ -181,7 +181,7 @@ def test_min_size_tiles_repaired(zp):
     want, wext = orc.parse_batch(a, o.astype(np.uint64), lens_np)
     ok_tiles = (want["err"].reshape(-1, 64) == 0).all(1).mean()
     assert 0.2 < ok_tiles < 0.9, ok_tiles
-    for shift in (0, 2):
+    for shift in (0, 2, 5, 12):
         got, gext = gpu_parse(zp, a, o, lens_np, base_shift=shift)
         assert_same(got, gext, want, wext)
     # the field checks around the checksums are reached: IPv4 version, total
@@ -554,7 +554,7 @@ def test_min_size_tiles(zp, layout):
         pa, po, pl = pack(frames)
         want, wext = orc.parse_batch(pa, po, pl)
         want_n = int((want["err"] != 0).sum())
-        for shift in range(4):
+        for shift in (0, 1, 2, 3, 4, 7, 8, 13, 15):   # every dword offset in a 16-B chunk
             got, gext = gpu_parse(zp, pa, po, pl, base_shift=shift)
             assert_same(got, gext, want, wext)
     else:
@@ -580,9 +580,9 @@ def test_min_size_tiles_small_batches(zp):
     tile whose 64 descriptors all name the same frame."""
     arena, offs, lens = zp.batch.generate("c1", 65, first=7, device=dev())
     a, o, l_ = arena.cpu().numpy(), offs.cpu().numpy(), lens.cpu().numpy()
-    for n in (1, 5, 64, 65):
+    for n in (1, 5, 63, 64, 65):
         want, wext = orc.parse_batch(a, o[:n], l_[:n])
-        for shift in (0, 1):
+        for shift in (0, 1, 6, 11):
             got, gext = gpu_parse(zp, a, o[:n], l_[:n], base_shift=shift)
             assert_same(got, gext, want, wext)
     same = np.full(64, o[3], np.uint64)
