@@ -40,6 +40,8 @@ def main():
     ap.add_argument("--membw", action="store_true")
     ap.add_argument("--no-base", action="store_true", help="time only --variants (PMC runs)")
     ap.add_argument("--columns", action="store_true", help="also time zp_extract_columns_device")
+    ap.add_argument("--col-variants", default="",
+                    help="A/B builds of zp_fields.hip (tools/variants/libzc_<name>.so), all columns")
     ap.add_argument("--c2cold", action="store_true",
                     help="c2 (1M x 64 B = 64 MiB, fits the 256 MiB MALL) warm vs cold: "
                          "8 rotating copies (512 MiB) so every launch reads from HBM")
@@ -172,6 +174,30 @@ def main():
                       f"{(nbytes + wbytes) / med / 1e6:6.0f} GB/s (frames + columns)  "
                       f"{n / med / 1e3:8.0f} Mpkt/s", flush=True)
                 del out
+        if args.col_variants:
+            zp.batch.parse_batch(arena, offs, lens, rec, ext, check=False)
+            out = zp.columns.extract(arena, offs, lens, rec)
+            ptrs = (ctypes.c_void_p * len(zp.columns.NAMES))()
+            for k, name in enumerate(zp.columns.NAMES):
+                ptrs[zp.columns.INDEX[name]] = out[name].data_ptr()
+            ref = {k: v.clone() for k, v in out.items()}
+            clibs = [("base", zp._lib.hip())] + [
+                (v, ctypes.CDLL(os.path.join(ROOT, "tools", "variants", f"libzc_{v}.so")))
+                for v in args.col_variants.split(",") if v]
+            res = {k: [] for k, _ in clibs}
+            s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+            for r in range(args.rounds):
+                for name, l in clibs:
+                    fn = lambda l=l: l.zp_extract_columns_device(
+                        ctypes.c_void_p(arena.data_ptr()), ctypes.c_void_p(offs.data_ptr()),
+                        ctypes.c_void_p(lens.data_ptr()), ctypes.c_void_p(rec.data_ptr()),
+                        ctypes.c_uint64(n), ptrs, s)
+                    res[name] += time_launches(fn, args.reps)
+                    if r == 0 and any(not torch.equal(ref[k], out[k]) for k in ref):
+                        print(f"  !! {name}: columns differ from base on {cfg}", flush=True)
+            for name, ms in res.items():
+                print(f"{cfg} columns[all] {name:>10}: {float(np.median(ms)):8.3f} ms", flush=True)
+            del out, ref
         del arena, offs, lens, rec, ext
         torch.cuda.empty_cache()
 

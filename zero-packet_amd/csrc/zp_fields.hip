@@ -61,9 +61,11 @@ __device__ __forceinline__ uint32_t hb(Hdr& h, uint32_t x) {
         h.xi = y >> 4;
         h.xc = fx_ld16(((uintptr_t)h.g & ~(uintptr_t)15) + 16u * h.xi);
     }
-    const uint32_t d = (y >> 2) & 3;
-    const uint32_t w = d == 0 ? h.xc.x : d == 1 ? h.xc.y : d == 2 ? h.xc.z : h.xc.w;
-    return (w >> (8 * (y & 3))) & 0xFFu;
+    // byte y & 15 of the chunk by shifts and one select (a select chain over
+    // the four dwords was lowered to a dynamically indexed scratch copy)
+    const uint64_t q = (y & 8) ? (((uint64_t)h.xc.w << 32) | h.xc.z)
+                               : (((uint64_t)h.xc.y << 32) | h.xc.x);
+    return (uint32_t)(q >> (8 * (y & 7))) & 0xFFu;
 }
 // Dword z (4-aligned, from A & ~15) of the staged window.
 __device__ __forceinline__ uint32_t hdw(const Hdr& h, uint32_t z) {
