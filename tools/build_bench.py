@@ -27,6 +27,9 @@ def main():
     ap.add_argument("--frames", type=int, default=1 << 22)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--variants", default="", help="tools/variants/libzb_<name>.so builds to A/B")
+    ap.add_argument("--payload", type=int, default=0,
+                    help="copy min(P, room) payload bytes from the data blob into each frame "
+                         "(set_payload(Some(..)); chains past the lane window: the group pass)")
     args = ap.parse_args()
     zp = importlib.import_module("zero-packet_amd")
     B = zp.builder
@@ -72,9 +75,15 @@ def main():
     l4["h"][icmp, 1] = 0
     for o in (eth, ip, l4):
         o["data_len"] = B.NO_DATA
+    pay = np.zeros(n, np.int64)
+    if args.payload:
+        start = np.where(tcp, 20, 8)
+        pay = np.minimum(args.payload, ln - 34 - start)
+        l4["data_len"] = pay.astype(np.uint32)
+        l4["data_off"] = 0
     t_ops = torch.from_numpy(ops.view(np.uint8)).to(d)
     t_start = torch.arange(0, 3 * n + 1, 3, dtype=torch.int32, device=d)
-    t_data = torch.zeros(16, dtype=torch.uint8, device=d)
+    t_data = torch.from_numpy(rng.integers(0, 256, max(16, args.payload), dtype=np.uint8)).to(d)
     res = torch.zeros((n, 8), dtype=torch.uint8, device=d)
     import ctypes
     libs = [("base", zp._lib.hip())]
@@ -110,9 +119,9 @@ def main():
         torch.cuda.synchronize()
         ms = float(np.median([a.elapsed_time(b) for a, b in ev]))
         nbytes = int(ln.sum())
-        hdr = n * 54
+        hdr = n * 54 + int(pay.sum())
         opb = int(t_ops.numel() + t_start.numel() * 4)
-        print(f"build c3 x {n} [{name}]: {ms:.3f} ms  {n / ms / 1e3:.0f} Mpkt/s  "
+        print(f"build c3 x {n}{f' payload {args.payload}' if args.payload else ''} [{name}]: {ms:.3f} ms  {n / ms / 1e3:.0f} Mpkt/s  "
               f"{(nbytes + hdr) / ms / 1e6:.0f} GB/s (frame read + header write; "
               f"{(nbytes + hdr + opb) / ms / 1e6:.0f} with the op reads)  errors {errs}",
               flush=True)

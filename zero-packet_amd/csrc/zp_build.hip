@@ -38,8 +38,8 @@ extern "C" char* zp__errbuf(void);
 #define ZB_OPS 4               // ops of a chain prefetched to LDS (longer chains read the rest)
 #endif
 #ifndef ZB_WPE
-#define ZB_WPE 5               // waves per SIMD: 96 VGPRs, 29 KB LDS per workgroup (measured 10 %
-#endif                         // faster than 4 waves with 8 prefetched ops)
+#define ZB_WPE 4               // waves per SIMD: 128 VGPRs (5 spilled at 96: 13 % slower on
+#endif                         // payload-copy chains), 29 KB LDS per workgroup
 #ifndef ZB_G
 #define ZB_G 16                // lanes per frame: a wave builds 64 / ZB_G frames side by side
 #endif
@@ -175,7 +175,33 @@ enum { ZB_M_COOP = 0, ZB_M_GLOBAL = 1, ZB_M_WIN = 2 };
 template <int MODE, typename P>
 __device__ void bcopy(BView<P>& v, uint32_t at, const uint8_t* src, uint32_t len, int lane) {
     if constexpr (MODE == ZB_M_COOP) {
-        for (uint32_t q = lane; q < len; q += ZB_G) v.b[at + q] = src[q];
+        // Aligned dword loads of the blob (address space 1: they cannot alias
+        // the LDS stores, so four are in flight per lane), byte stores to the
+        // staged frame. One byte per lane and trip was 20 % slower on
+        // payload-copy chains (tools/build_bench.py --payload).
+        const uintptr_t sa = (uintptr_t)src, sb = sa & ~(uintptr_t)3;
+        const uint32_t sh = (uint32_t)(sa & 3);
+        const ZP_GLOBAL uint32_t* g32 = (const ZP_GLOBAL uint32_t*)sb;
+        for (uint32_t k0 = lane; 4 * k0 < len; k0 += 4 * ZB_G) {
+            uint32_t d[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t k = k0 + u * ZB_G;
+                uint32_t lo = 0, hi = 0;
+                if (4 * k < len) {
+                    lo = g32[k];
+                    if (sh && sb + 4 * (k + 1) < sa + len) hi = g32[k + 1];
+                }
+                d[u] = __builtin_amdgcn_alignbyte(hi, lo, sh);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t k = k0 + u * ZB_G;
+#pragma unroll
+                for (uint32_t b = 0; b < 4; ++b)
+                    if (4 * k + b < len) v.b[at + 4 * k + b] = (uint8_t)(d[u] >> (8 * b));
+            }
+        }
         wave_sync();
     } else {
         for (uint32_t q = 0; q < len; ++q) v.b[at + q] = src[q];
