@@ -137,6 +137,7 @@ struct BView {
     P b;
     uint32_t n;
     bool writer;      // this lane stores
+    uint32_t lim = ~0u;   // ZB_M_WIN: blob copies stop at this frame offset (the rest: HBM)
 };
 
 template <typename P>
@@ -203,6 +204,11 @@ __device__ void bcopy(BView<P>& v, uint32_t at, const uint8_t* src, uint32_t len
             }
         }
         wave_sync();
+    } else if constexpr (MODE == ZB_M_WIN) {
+        // the part inside the lane's window; a payload past it goes to HBM
+        // after the chain (zp_build_fast_kernel)
+        const uint32_t m = at >= v.lim ? 0u : (v.lim - at < len ? v.lim - at : len);
+        for (uint32_t q = 0; q < m; ++q) v.b[at + q] = src[q];
     } else {
         for (uint32_t q = 0; q < len; ++q) v.b[at + q] = src[q];
     }
@@ -686,10 +692,11 @@ struct WinCsum {
     uint4 tail;                       // the frame's last chunk (original bytes)
     uintptr_t ga;
     uint32_t shift, len, nchw, fsum;
+    uint32_t pdelta;                  // V change of a payload copied past the window
     uint32_t vorig[ZP_WIN_CH];
     __device__ uint16_t csum(uint32_t l4, uint32_t acc) const {
         const uint32_t y4 = l4 + shift, c4 = y4 >> 4;
-        uint32_t vall = fsum, before = 0;
+        uint32_t vall = fsum + pdelta, before = 0;
 #pragma unroll
         for (uint32_t c = 0; c < ZP_WIN_CH; ++c) {
             if (c < nchw) {
@@ -714,8 +721,12 @@ struct WinCsum {
 // Upper bound of the bytes a chain can read or write (from its ops alone;
 // the offsets the writers derive from the buffer are the values the chain
 // itself wrote: ihl, data offset, extension lengths).
-__device__ uint32_t chain_extent(const OpGlobal& ops, uint32_t nops) {
+__device__ uint32_t chain_extent(const OpGlobal& ops, uint32_t nops, uint32_t* pay_at = nullptr,
+                             uint32_t* pay_len = nullptr) {
+    // With pay_at: the final L4 op's payload copy is left out of the extent
+    // and reported as [*pay_at, *pay_at + *pay_len) (frame offsets).
     uint32_t hl = 0, top = 0;
+    if (pay_at) { *pay_at = 0; *pay_len = 0; }
     for (uint32_t k = 0; k < nops; ++k) {
         const zp_build_op o = ops.get(k);
         const uint32_t dl = o.data_len != ZP_BUILD_NO_DATA ? o.data_len : 0u;
@@ -735,9 +746,16 @@ __device__ uint32_t chain_extent(const OpGlobal& ops, uint32_t nops) {
         case ZP_B_AUTH: ext = 12 + dl; adv = ((uint32_t)o.b[1] + 2) * 4; break;
         case ZP_B_TCP: {
             const uint32_t st = (o.b[0] & 15u) * 4;
-            ext = st + dl > 20 ? st + dl : 20; adv = st; break;
+            ext = st + dl > 20 ? st + dl : 20; adv = st;
+            if (pay_at && k + 1 == nops && dl) {
+                *pay_at = hl + st; *pay_len = dl; ext = st > 20 ? st : 20;
+            }
+            break;
         }
-        default: ext = 8 + dl; adv = 8; break;           // UDP, ICMPv4, ICMPv6
+        default:                                         // UDP, ICMPv4, ICMPv6
+            ext = 8 + dl; adv = 8;
+            if (pay_at && k + 1 == nops && dl) { *pay_at = hl + 8; *pay_len = dl; ext = 8; }
+            break;
         }
         top = hl + ext > top ? hl + ext : top;
         hl += adv;
@@ -749,6 +767,64 @@ __device__ uint32_t chain_extent(const OpGlobal& ops, uint32_t nops) {
 #ifndef ZB_FAST_WPE
 #define ZB_FAST_WPE 1
 #endif
+#ifndef ZB_LANE_PAY
+#define ZB_LANE_PAY 1          // payload copies past the window on the lane path
+#endif
+
+// V (little-endian words at even ARENA addresses) and the plain byte sum B of
+// global bytes [a0, a1): aligned dword loads, ZB_PAY_DW in flight.
+#ifndef ZB_PAY_DW
+#define ZB_PAY_DW 8
+#endif
+__device__ __forceinline__ void gsum_vb(uintptr_t a0, uintptr_t a1, uint32_t& V, uint32_t& B) {
+    V = 0;
+    B = 0;
+    const uintptr_t d0 = a0 & ~(uintptr_t)3;
+    for (uintptr_t d = d0; d < a1; d += 4 * ZB_PAY_DW) {
+        uint32_t x[ZB_PAY_DW];
+#pragma unroll
+        for (int u = 0; u < ZB_PAY_DW; ++u) {
+            const uintptr_t a = d + 4u * u;
+            x[u] = a < a1 ? *(const ZP_GLOBAL uint32_t*)a : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < ZB_PAY_DW; ++u) {
+            const uintptr_t a = d + 4u * u;
+            if (a < a1) {
+                const int lo = a0 > a ? (int)(a0 - a) : 0;
+                const int hi = a1 - a < 4 ? (int)(a1 - a) : 4;
+                const uint32_t m = x[u] & byte_mask(0, lo, hi);
+                V = sad16(m, V);
+                B = __builtin_amdgcn_sad_u8(m, 0u, B);
+            }
+        }
+    }
+}
+
+// Copies global bytes [src, src + n) to [dst, dst + n) (n < 64 KiB, no
+// overlap): byte stores up to a 4-aligned destination, then 4 ZB_PAY_DW bytes
+// per trip from aligned source dwords, then byte stores.
+__device__ __forceinline__ void gcopy(uintptr_t dst, uintptr_t src, uint32_t n) {
+    uint32_t q = 0;
+    for (; q < n && ((dst + q) & 3); ++q)
+        *(ZP_GLOBAL uint8_t*)(dst + q) = *(const ZP_GLOBAL uint8_t*)(src + q);
+    const uintptr_t send = src + n;
+    for (; q + 4 * ZB_PAY_DW <= n; q += 4 * ZB_PAY_DW) {
+        const uintptr_t s0 = src + q, sb = s0 & ~(uintptr_t)3;
+        const uint32_t sh = (uint32_t)(s0 & 3);
+        uint32_t x[ZB_PAY_DW + 1];
+#pragma unroll
+        for (int k = 0; k <= ZB_PAY_DW; ++k) {
+            const uintptr_t a = sb + 4u * k;
+            x[k] = (k < ZB_PAY_DW || (sh && a < send)) ? *(const ZP_GLOBAL uint32_t*)a : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < ZB_PAY_DW; ++k)
+            *(ZP_GLOBAL uint32_t*)(dst + q + 4u * k) = __builtin_amdgcn_alignbyte(x[k + 1], x[k], sh);
+    }
+    for (; q < n; ++q)
+        *(ZP_GLOBAL uint8_t*)(dst + q) = *(const ZP_GLOBAL uint8_t*)(src + q);
+}
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZB_FAST_WPE)))
 zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs,
                      const uint32_t* __restrict__ lens, uint64_t n,
@@ -793,11 +869,22 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
     const uint64_t i = t * 64 + lane;
     uint32_t o0 = 0, nops = 0;
     bool fast = false;
+    bool pay = false;                                  // payload bytes past the window
+    uint32_t pay_at = 0, pay_len = 0;
     if (s.live) {
         o0 = pf0;
         const uint32_t o1 = pf1;
         nops = o1 >= o0 ? o1 - o0 : 0u;
+#if ZB_LANE_PAY
+        // A final payload copy may reach past the window: the headers must
+        // fit it; the copy's bytes past it go straight to HBM after the chain.
+        if (o1 >= o0 && len >= 64 && !s.giant) {
+            fast = chain_extent(OpGlobal{ops + o0}, nops, &pay_at, &pay_len) <= s.wlen;
+            pay = fast && pay_len && pay_at + pay_len > s.wlen;
+        }
+#else
         fast = o1 >= o0 && len >= 64 && !s.giant && chain_extent(OpGlobal{ops + o0}, nops) <= s.wlen;
+#endif
         if (!fast) {
             zp_build_result r;
             r.header_len = 0; r.err = (uint8_t)ZB_PENDING; r.ops_done = 0; r.reserved = 0;
@@ -817,6 +904,7 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
         wc.nchw = nch < ZP_WIN_CH ? nch : ZP_WIN_CH;
         wc.fsum = lds.cend[s.rank] - (s.rank ? lds.cend[s.rank - 1] : 0u);
         wc.tail = tail[rank];
+        wc.pdelta = 0;
         ptail = tail[(rank - 1) & 63u];
 #pragma unroll
         for (uint32_t c = 0; c < ZP_WIN_CH; ++c) {
@@ -836,6 +924,45 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
         }
         wc.region = region;
         BView<uint8_t ZB_LDSP*> v{region + s.shift, len, true};
+#if ZB_LANE_PAY
+        if (pay) {
+            v.lim = s.wlen;
+            // The L4 checksum sees the payload bytes past the window in place
+            // of the frame's: V(blob part, at its destination's parity) -
+            // V(original bytes). A copy that does not fit the frame fails in
+            // the chain before any byte is written; nothing to add then.
+            const uint32_t q0 = s.wlen > pay_at ? s.wlen : pay_at, pe = pay_at + pay_len;
+            if (pe <= len) {
+                const uintptr_t src = (uintptr_t)data + og.get(nops - 1).data_off + (q0 - pay_at);
+                // V of the original bytes [q0, pe): read where that is
+                // shorter than the rest of the frame; otherwise the stream's
+                // sum of the frame's chunks minus the window's chunks, the
+                // frame's bytes between the window and q0 and from pe to its
+                // end, and the bytes past its end in its last chunk, from the
+                // kept original chunk (in HBM they are the next frame's, which
+                // its lane may be rewriting). Only this lane writes [q0, pe),
+                // and only after the chain.
+                uint32_t Vo, Bo, Vb, Bb;
+                if (pe - q0 <= len - pe) {
+                    gsum_vb(s.ga + q0, s.ga + pe, Vo, Bo);
+                } else {
+                    uint32_t Vw = 0;
+#pragma unroll
+                    for (uint32_t c = 0; c < ZP_WIN_CH; ++c) Vw += wc.vorig[c];
+                    const uint32_t he = (len + s.shift) & 15u;
+                    uint32_t Vh, Bh, Vt, Bt;
+                    gsum_vb(s.ga + s.wlen, s.ga + q0, Vh, Bh);
+                    gsum_vb(s.ga + pe, s.ga + len, Vt, Bt);
+                    const uint32_t Vx = he ? range_sum(wc.tail, he, 16u) : 0u;
+                    Vo = wc.fsum - Vw - Vh - Vt - Vx;
+                }
+                gsum_vb(src, src + (pe - q0), Vb, Bb);
+                const uint32_t O = (Vb - Bb) / 255u, E = Bb - O;   // blob bytes at odd / even addresses
+                const uint32_t Vd = ((src ^ (s.ga + q0)) & 1) ? O + 256u * E : Vb;
+                wc.pdelta = Vd - Vo;
+            }
+        }
+#endif
         err = run_chain<ZB_M_WIN>(v, (const uint8_t ZB_LDSP*)nullptr, s.shift, og, nops, wc,
                                   data, lane, &hl, &done, &hw);
     }
@@ -850,6 +977,9 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
     // frame ends exactly here and its lane writes nothing there.
     const uintptr_t a0 = s.ga & ~(uintptr_t)15;
     const uint32_t sh = s.shift;
+#if ZB_LANE_PAY
+    const bool pay_go = pay && err == 0;               // the chain copied the payload
+#endif
     const uint32_t hwc = hw < s.wlen ? hw : s.wlen;               // hw <= extent <= wlen
     uint32_t end = fast ? sh + hwc : sh;                          // window coordinates
 #ifndef ZB_NO_SECTOR_WB
@@ -860,7 +990,11 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
         if (hwc && e1 <= sh + s.wlen) end = e1;                   // bytes in the window
     }
     // the previous lane's frame and where its writes end (all lanes active)
+#if ZB_LANE_PAY
+    const uintptr_t wend = pay_go ? s.ga + pay_at + pay_len : a0 + end;
+#else
     const uintptr_t wend = a0 + end;
+#endif
     const uint32_t pl = lane ? (uint32_t)lane - 1u : 0u;
     const uintptr_t pA = ((uintptr_t)bperm((uint32_t)(s.ga >> 32), pl) << 32) |
                          bperm((uint32_t)s.ga, pl);
@@ -892,6 +1026,13 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
                 *(ZP_GLOBAL uint8_t*)(a0 + b) = region[b];
         }
     }
+#if ZB_LANE_PAY
+    if (pay_go) {                                      // the payload past the window
+        const uint32_t q0 = s.wlen > pay_at ? s.wlen : pay_at;
+        const uintptr_t src = (uintptr_t)data + og.get(nops - 1).data_off + (q0 - pay_at);
+        gcopy(s.ga + q0, src, pay_at + pay_len - q0);
+    }
+#endif
     if (!fast) return;
     zp_build_result r;
     r.header_len = hl;
