@@ -721,7 +721,7 @@ struct WinCsum {
 // Upper bound of the bytes a chain can read or write (from its ops alone;
 // the offsets the writers derive from the buffer are the values the chain
 // itself wrote: ihl, data offset, extension lengths).
-__device__ uint32_t chain_extent(const OpGlobal& ops, uint32_t nops, uint32_t* pay_at = nullptr,
+__device__ __forceinline__ uint32_t chain_extent(const OpGlobal& ops, uint32_t nops, uint32_t* pay_at = nullptr,
                              uint32_t* pay_len = nullptr) {
     // With pay_at: the final L4 op's payload copy is left out of the extent
     // and reported as [*pay_at, *pay_at + *pay_len) (frame offsets).
