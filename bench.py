@@ -6,9 +6,18 @@ One step = one zp_parse_batch_device launch over the whole per-GPU batch
 (inputs already resident in HBM). Default workload: BASELINE config 3 — 16M
 IPv4 frames, TCP/UDP/ICMPv4, lengths U[64,1500] (~13.1 GB, far past the
 256 MiB Infinity Cache, so every step streams from HBM). Multi-GPU: one
-process per GPU (torchrun), each parses its own 16M-frame shard (packets
+process per GPU, each parses its own 16M-frame shard (packets
 rank*P .. rank*P+P-1; weak scaling, no data-path collective). Rank 0 prints
 one JSON line.
+
+`python bench.py --gpus N` with N > 1 and no launcher around it starts the N
+ranks itself: the parent spawns `torch.distributed.run --nproc-per-node N`
+on this same command line before it touches the GPU, and relays rank 0's
+JSON line. Under a launcher, --gpus must equal WORLD_SIZE.
+
+--config c5 without --packets is config 5 itself: the 256M-frame IMIX stream
+split into N contiguous shards, rank r parsing the r-th (strong scaling; at
+N = 1 the whole 95 GB batch on one GPU).
 
 Reported next to the GPU number:
   roofline      algorithmic bytes (sum of frame lengths) / mean kernel time
@@ -43,11 +52,56 @@ WORKLOADS = {
     "c6": "16M mixed: c3/c4/c5 shapes + 1/16 ARP per packet (not a BASELINE config)",
 }
 DEFAULT_PACKETS = {"c1": 1 << 20, "c2": 1 << 20, "c3": 1 << 24, "c4": 1 << 24,
-                   "c5": (1 << 28) // 8, "c6": 1 << 24}
+                   "c6": 1 << 24}
+C5_TOTAL = 1 << 28          # config 5: one 256M-frame stream over all ranks
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def host_cores():
+    """CPU threads this process may use: the affinity mask, capped by the
+    cgroup CPU quota when there is one (a GPU box shows the whole machine in
+    its affinity mask but grants a share of it)."""
+    n = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(period)
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            p = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / p
+        except (OSError, ValueError):
+            pass
+    threads = n if quota is None else max(1, min(n, int(quota)))
+    return threads, n, quota
+
+
+def spawn_ranks(n):
+    """Runs this command line under torch.distributed.run with n ranks and
+    relays rank 0's JSON line; returns the launcher's exit code. Called before
+    anything touches the GPU (no exec from a GPU-initialised process)."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr=127.0.0.1", f"--master-port={port}",
+           os.path.abspath(__file__)] + sys.argv[1:]
+    log(f"[bench] spawning {n} ranks: {' '.join(cmd)}")
+    p = subprocess.run(cmd, stdout=subprocess.PIPE, text=True)
+    for line in p.stdout.splitlines():
+        if line.startswith("{"):
+            print(line, flush=True)
+        else:
+            log(line)
+    return p.returncode
 
 
 def pmc_traffic(config, frames, nbytes):
@@ -63,7 +117,7 @@ def pmc_traffic(config, frames, nbytes):
 
 
 def cpu_baseline(zp, arena, offs, lens, sample_pkts, min_seconds):
-    """Times the oracle (C port, all threads of this process' CPU share) on the
+    """Times the oracle (C port, every core of this process' CPU share) on the
     first `sample_pkts` frames, copied to host memory."""
     from tests import oracle as orc   # the checker, used here only as the baseline
     m = min(sample_pkts, offs.numel())
@@ -71,7 +125,8 @@ def cpu_baseline(zp, arena, offs, lens, sample_pkts, min_seconds):
     ln = lens[:m].cpu().numpy().astype(np.uint32)
     end = int(o[-1] + ln[-1])
     a = arena[:end].cpu().numpy()
-    threads = int(os.environ.get("ZP_CPU_THREADS", min(16, os.cpu_count() or 1)))
+    cores, visible, quota = host_cores()
+    threads = int(os.environ.get("ZP_CPU_THREADS", cores))
     orc.parse_batch(a, o[:1024], ln[:1024], threads)          # warm
     reps, t0 = 0, time.perf_counter()
     while True:
@@ -93,6 +148,7 @@ def cpu_baseline(zp, arena, offs, lens, sample_pkts, min_seconds):
             break
     sec1 = dt1 / reps1
     return {"value": round(m / sec / 1e6, 3), "unit": "Mpkt/s", "cores": threads,
+            "cpus_in_affinity_mask": visible, "cgroup_cpu_quota": quota,
             "kind": "port", "gb_per_s": round(float(ln.sum()) / sec / 1e9, 3),
             "value_1core": round(m1 / sec1 / 1e6, 3),
             "gb_per_s_1core": round(float(ln[:m1].sum()) / sec1 / 1e9, 3),
@@ -137,6 +193,16 @@ def main():
     ap.add_argument("--no-pcie", action="store_true")
     args = ap.parse_args()
 
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:
+            sys.exit(spawn_ranks(args.gpus))
+    elif int(os.environ["WORLD_SIZE"]) != args.gpus:
+        log(f"[bench] --gpus {args.gpus} but the launcher started "
+            f"WORLD_SIZE={os.environ['WORLD_SIZE']} ranks")
+        sys.exit(2)
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -161,9 +227,15 @@ def main():
                 dist.barrier(device_ids=[local_dev])
 
     zp = importlib.import_module("zero-packet_amd")
-    n = args.packets or DEFAULT_PACKETS[args.config]
+    if args.config == "c5" and not args.packets:
+        # config 5: contiguous 1/world shards of one 256M-frame stream
+        first, end = C5_TOTAL * rank // world, C5_TOTAL * (rank + 1) // world
+        n, job_frames, scaling = end - first, C5_TOTAL, "strong"
+    else:
+        n = args.packets or DEFAULT_PACKETS[args.config]
+        first, job_frames, scaling = rank * n, n * world, "weak"
     t0 = time.perf_counter()
-    arena, offs, lens = zp.batch.generate(args.config, n, first=rank * n, device=dev)
+    arena, offs, lens = zp.batch.generate(args.config, n, first=first, device=dev)
     records = torch.empty((n, 16), dtype=torch.uint8, device=dev)
     ext = torch.empty((2, n, 16), dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
@@ -196,26 +268,29 @@ def main():
     elapsed = time.perf_counter() - t0
     kms = [a.elapsed_time(b) for a, b in ev]
     t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if shared else dev)
+    job_bytes = torch.tensor([total_bytes], dtype=torch.int64, device="cpu" if shared else dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(job_bytes, op=dist.ReduceOp.SUM)
     elapsed = float(t.item())
+    job_bytes = int(job_bytes.item())
 
     traffic, traffic_src = pmc_traffic(args.config, n, total_bytes)
     ms_step = elapsed / args.steps * 1e3
-    pkts = n * world * args.steps
-    mpkts = pkts / elapsed / 1e6
-    gbs = total_bytes * world * args.steps / elapsed / 1e9
+    mpkts = job_frames * args.steps / elapsed / 1e6
+    gbs = job_bytes * args.steps / elapsed / 1e9
     kmean = float(np.mean(kms))
     achieved = total_bytes / (kmean * 1e-3) / 1e9
 
     out = {
         "metric": METRIC, "value": round(mpkts, 2), "unit": "Mpkt/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": "u8",
         "data": "synthetic (zp_gen: deterministic frames with valid checksums)",
         "gb_per_s": round(gbs, 2),
         "config": {"workload": WORKLOADS[args.config], "config": args.config,
                    "frames_per_gpu": n, "bytes_per_gpu": total_bytes,
+                   "job_frames": job_frames, "job_bytes": job_bytes,
                    "mean_frame_bytes": round(total_bytes / n, 2),
                    "parallelism": f"dp{world} (independent shards, no collective)"
                                   + (" [ranks share GPUs: rehearsal only]" if shared else "")},

@@ -447,6 +447,12 @@ def test_gpu_builder_descriptor_bounds_refused(zp):
         zp.builder.BuildBatch().add(chain).run(
             arena, torch.tensor([0], dtype=torch.int32, device=d),
             torch.tensor([64], dtype=torch.int32, device=d))
+    # overlapping (and duplicated) frames are refused: the kernel writes them
+    two = zp.builder.BuildBatch().add(chain).add(chain)
+    for offs in ([0, 10], [20, 20], [25, 0]):
+        with pytest.raises(ValueError, match="overlap"):
+            two.run(arena, torch.tensor(offs, dtype=torch.int64, device=d),
+                    torch.tensor([30, 30], dtype=torch.int32, device=d))
     assert int(arena.sum().item()) == 0                  # nothing written
     res = zp.builder.BuildBatch().add(chain).run(
         arena, torch.tensor([36], dtype=torch.int64, device=d),

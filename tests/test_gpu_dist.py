@@ -39,3 +39,22 @@ def test_bench_two_ranks():
     # value = frames of all ranks / max-over-ranks time
     assert abs(r["value"] - 2 * n * 3 / (r["ms_per_step"] * 3 * 1e-3) / 1e6) < 0.02 * r["value"]
     assert "cpu_baseline" not in r            # rank 0 at N=1 only
+
+
+def test_bench_spawns_ranks_itself():
+    """`python bench.py --gpus 2` with no launcher around it (the driver's
+    command) starts both ranks itself and reports n_gpus == 2."""
+    n = 1 << 20
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3",
+           "--warmup", "1", "--packets", str(n)]
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env["OMP_NUM_THREADS"] = "1"
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    r = json.loads(lines[0])
+    assert r["n_gpus"] == 2 and r["scaling"] == "weak"
+    assert r["config"]["frames_per_gpu"] == n and r["config"]["job_frames"] == 2 * n
+    assert abs(r["value"] - 2 * n * 3 / (r["ms_per_step"] * 3 * 1e-3) / 1e6) < 0.02 * r["value"]

@@ -8,9 +8,13 @@
        is valid where the record's ZP_F_EXT / ZP_F_INNER_EXT bit is set)
 
 parse_batch() enqueues the HIP kernel on torch's current stream of the
-tensors' device (zp_parse_batch_device). No CPU fallback: non-CUDA tensors or
-a missing libzp_hip.so raise.
+tensors' device, or on `stream` (zp_parse_batch_device). By default
+(check=True) it first validates the descriptors with one device reduction on
+that same stream and reads the result back, so the default call SYNCHRONISES
+with the stream; check=False makes it enqueue-only. No CPU fallback: non-CUDA
+tensors or a missing libzp_hip.so raise.
 """
+import contextlib
 import ctypes
 
 import numpy as np
@@ -33,7 +37,7 @@ def _need_cuda(*ts):
             raise RuntimeError("zero-packet_amd batch API needs device tensors (no CPU fallback)")
 
 
-def check_batch(arena, offs, lens, outs=(), bounds=True):
+def check_batch(arena, offs, lens, outs=(), bounds=True, stream=None):
     """Validates a device batch before a kernel reads it: dtypes, shapes,
     contiguity and device of every tensor, and (bounds=True) that every frame
     lies inside the arena: 0 <= offs[i], 0 <= lens[i], offs[i] + lens[i] <=
@@ -41,7 +45,10 @@ def check_batch(arena, offs, lens, outs=(), bounds=True):
     past the arena faults the GPU), so this is the Python API's guard; it
     costs one device reduction and one synchronisation. `outs` holds
     (tensor, row_bytes) pairs of outputs ([n, row_bytes] uint8, or any
-    contiguous tensor of n * row_bytes bytes)."""
+    contiguous tensor of n * row_bytes bytes). The reduction runs on `stream`
+    (a hipStream_t as int, the stream the kernel will be launched on) when
+    given, so descriptors still being produced on it are read after they are
+    written."""
     _need_cuda(arena, offs, lens)
     n = offs.numel()
     if arena.dtype != torch.uint8 or arena.dim() != 1 or not arena.is_contiguous():
@@ -62,9 +69,12 @@ def check_batch(arena, offs, lens, outs=(), bounds=True):
         if t.device != dev:
             raise ValueError(f"descriptor tensor on {t.device}, arena on {dev}")
     if bounds and n:
-        lo = torch.minimum(offs.min(), lens.min().to(torch.int64))
-        hi = (offs + lens.to(torch.int64)).max()
-        lo, hi = torch.stack([lo, hi]).tolist()
+        on = (torch.cuda.stream(torch.cuda.ExternalStream(int(stream), device=dev))
+              if stream is not None else contextlib.nullcontext())
+        with on:
+            lo = torch.minimum(offs.min(), lens.min().to(torch.int64))
+            hi = (offs + lens.to(torch.int64)).max()
+            lo, hi = torch.stack([lo, hi]).tolist()
         if lo < 0:
             raise ValueError("negative frame offset or length")
         if hi > arena.numel():
@@ -83,13 +93,16 @@ def alloc_outputs(n, device, records=None, ext=None):
 
 def parse_batch(arena, offs, lens, records=None, ext=None, stream=None, check=True):
     """Parses every frame; returns (records, ext) as uint8 device tensors.
-    check=False skips the descriptor bounds reduction (check_batch) for callers
-    that validated the batch already; shapes and devices are always checked."""
+    check=True (default) runs the descriptor bounds reduction (check_batch) on
+    the launch stream and waits for it, so the call synchronises; check=False
+    skips it for callers that validated the batch already and makes the call
+    enqueue-only. Shapes and devices are always checked."""
     n = offs.numel()
     dev = arena.device
     if arena.is_cuda:
         records, ext = alloc_outputs(n, dev, records, ext)
-    check_batch(arena, offs, lens, ((records, RECORD_BYTES), (ext, 2 * EXT_BYTES)), bounds=check)
+    check_batch(arena, offs, lens, ((records, RECORD_BYTES), (ext, 2 * EXT_BYTES)), bounds=check,
+                stream=stream)
     s = ctypes.c_void_p(stream) if stream is not None else _stream_ptr(dev)
     rc = _lib.hip().zp_parse_batch_device(arena.data_ptr(), offs.data_ptr(), lens.data_ptr(), n,
                                           records.data_ptr(), ext.data_ptr(), s)

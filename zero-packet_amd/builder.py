@@ -16,6 +16,7 @@ Errors do not raise per frame: results["err"] holds the zp_build_err code
 (error_string() gives the reference's message) and, as in the reference, the
 bytes written before the failing step stay in the buffer.
 """
+import contextlib
 import ctypes
 
 import numpy as np
@@ -125,6 +126,27 @@ class Chain:
                         dst=dest_addr, b={0: icmp_type, 1: icmp_code})
 
 
+def check_disjoint(offs, lens, stream=None):
+    """Raises ValueError unless the non-empty frames [offs[i], offs[i] +
+    lens[i]) are pairwise disjoint (an empty frame holds no byte, and its
+    chain fails at its first step without writing). One device sort and
+    reduction on `stream`, then a sync."""
+    if offs.numel() < 2:
+        return
+    dev = offs.device
+    on = (torch.cuda.stream(torch.cuda.ExternalStream(int(stream), device=dev))
+          if stream is not None else contextlib.nullcontext())
+    with on:
+        live = lens > 0
+        o, ln = offs[live], lens[live].to(torch.int64)
+        so, order = torch.sort(o)
+        ends = so + ln[order]
+        bad = int((ends[:-1] > so[1:]).sum().item())
+    if bad:
+        raise ValueError(f"{bad} frame(s) overlap the next frame in address order: "
+                         "zp_build_batch_device needs disjoint frames")
+
+
 class BuildBatch:
     """Chains for many frames, packed into the C-ABI arrays."""
 
@@ -171,8 +193,12 @@ class BuildBatch:
         """Executes every chain in place on the device tensors; returns the
         results (numpy RESULT_DTYPE [n])."""
         # the kernel writes into [offs[i], offs[i] + lens[i]) of the arena:
-        # dtypes, devices and bounds are checked before it runs (check_batch)
-        check_batch(arena, offs, lens)
+        # dtypes, devices and bounds are checked before it runs (check_batch),
+        # and so is the header's precondition that frames do not overlap (a
+        # lane also completes the 64-B sector it shares with the frame before
+        # its own, so overlapping frames would race on bytes of both)
+        check_batch(arena, offs, lens, stream=stream)
+        check_disjoint(offs, lens, stream)
         n = offs.numel()
         if n != len(self.chains):
             raise ValueError(f"{len(self.chains)} chains for {n} frames")

@@ -31,12 +31,14 @@ def count(records, counts=None, stream=None):
     `counts` (int64 [COUNT] device tensor, zeroed when not given)."""
     if not records.is_cuda:
         raise RuntimeError("stats.count needs device records (no CPU fallback)")
-    if records.dim() != 2 or records.shape[1] != RECORD_BYTES or not records.is_contiguous():
+    if (records.dtype != torch.uint8 or records.dim() != 2 or records.shape[1] != RECORD_BYTES
+            or not records.is_contiguous()):
         raise ValueError("records must be a contiguous uint8 [n, 16] tensor")
     if counts is None:
         counts = torch.zeros(COUNT, dtype=torch.int64, device=records.device)
-    if counts.numel() != COUNT or counts.dtype != torch.int64 or counts.device != records.device:
-        raise ValueError(f"counts must be an int64 [{COUNT}] tensor on {records.device}")
+    if (counts.numel() != COUNT or counts.dtype != torch.int64 or counts.device != records.device
+            or not counts.is_contiguous()):
+        raise ValueError(f"counts must be a contiguous int64 [{COUNT}] tensor on {records.device}")
     s = ctypes.c_void_p(stream) if stream is not None else \
         ctypes.c_void_p(torch.cuda.current_stream(records.device).cuda_stream)
     _lib.check(_lib.hip().zp_stats_device(records.data_ptr(), records.shape[0], counts.data_ptr(),
