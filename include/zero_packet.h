@@ -27,7 +27,10 @@
 extern "C" {
 #endif
 
-#define ZP_ABI_VERSION 2   /* 2: 16-B record, extension chains in the ext side array */
+#define ZP_ABI_VERSION 3   /* 2: 16-B record, extension chains in the ext side array;
+                              3: reader-accessor error codes 36-37 (ZP_ERR_COUNT 38,
+                                 ZP_STATS_COUNT 62), standalone readers and the
+                                 checksum primitives (zp_reader_new, zp_*checksum*) */
 
 /* ------------------------------------------------------------------------- */
 /* Per-packet parse error codes. One code per DISTINCT reference error string */
@@ -73,7 +76,10 @@ typedef enum zp_err {
     ZP_ERR_ICMPV6_TYPE = 33,          /* parser.rs:298                          */
     ZP_ERR_IPV4_L4_CHECKSUM = 34,     /* parser.rs:329                          */
     ZP_ERR_IPV6_L4_CHECKSUM = 35,     /* parser.rs:357                          */
-    ZP_ERR_COUNT = 36
+    /* Errors of the reader accessors only (parse() never returns them):    */
+    ZP_ERR_TCP_HDR_EXCEEDS = 36,      /* tcp.rs:227,239 (header()/payload())    */
+    ZP_ERR_OPTIONS_DATA_EXCEEDS = 37, /* options.rs:115 (options())             */
+    ZP_ERR_COUNT = 38
 } zp_err;
 
 /* ------------------------------------------------------------------------- */
@@ -210,6 +216,61 @@ int zp_parse_batch_host_multi(zp_ctx* const* ctxs, int nctx, const uint8_t* aren
  * negative value on HIP failure. */
 int zp_parse_one(zp_ctx* ctx, const uint8_t* frame, uint64_t len,
                  zp_record* record, zp_ext_offsets ext[2]);
+
+/* ------------------------------------------------------------------------- */
+/* Standalone readers and the checksum primitives.                           */
+/* The reference's second usage (README.md:110-115) builds a reader directly */
+/* over a slice: TcpReader::new(&packet[off..])? and reads its fields. Every  */
+/* reader's `new` is a checked constructor returning Result (the minimum     */
+/* slice length; Ethernet also the VLAN tagging; IPv6 also the extension    */
+/* walk, ipv6.rs:159). These are host-side views over host bytes, like the  */
+/* reference's: one slice, no batch, no device. The batch parse stays the   */
+/* device path above.                                                        */
+/* ------------------------------------------------------------------------- */
+typedef enum zp_reader_kind {
+    ZP_READER_ETHERNET = 0,  /* EthernetReader::new               ethernet.rs:141 */
+    ZP_READER_ARP = 1,       /* ArpReader::new                    arp.rs:130      */
+    ZP_READER_IPV4 = 2,      /* IPv4Reader::new                   ipv4.rs:138     */
+    ZP_READER_IPV6 = 3,      /* IPv6Reader::new (+ extension walk) ipv6.rs:147-167 */
+    ZP_READER_OPTIONS = 4,   /* OptionsHeaderReader::new          options.rs:83   */
+    ZP_READER_ROUTING = 5,   /* RoutingHeaderReader::new          routing.rs:107  */
+    ZP_READER_FRAGMENT = 6,  /* FragmentHeaderReader::new         fragment.rs:97  */
+    ZP_READER_AUTH = 7,      /* AuthenticationHeaderReader::new   authentication.rs:105 */
+    ZP_READER_TCP = 8,       /* TcpReader::new                    tcp.rs:141      */
+    ZP_READER_UDP = 9,       /* UdpReader::new                    udp.rs:103      */
+    ZP_READER_ICMPV4 = 10,   /* Icmpv4Reader::new                 icmpv4.rs:92    */
+    ZP_READER_ICMPV6 = 11,   /* Icmpv6Reader::new                 icmpv6.rs:89    */
+    ZP_READER_KIND_COUNT = 12
+} zp_reader_kind;
+
+/* What a successful constructor computed besides the slice itself. */
+typedef struct zp_reader_info {
+    uint32_t header_len;     /* Ethernet: 14/18/22 (calculate_header_len,      */
+                             /* ethernet.rs:155-179); 0 for the other kinds    */
+    uint32_t flags;          /* IPv6: ZP_F_EXT when extension_headers is Some, */
+                             /* ZP_F_EXT_SLOT(k) per present slot; else 0      */
+    uint8_t  final_nh;       /* IPv6: final_next_header() (ipv6.rs:219-227)    */
+    uint8_t  reserved[3];
+    zp_ext_offsets ext;      /* IPv6: extension_headers_len (ext.len) and the  */
+                             /* slot offsets, relative to the IPv6 payload     */
+} zp_reader_info;
+
+/* XReader::new(&bytes[..len]) of reader `kind`. Returns ZP_OK (info filled,
+ * when not NULL) or the zp_err code of the reference's Err, whose string is
+ * zp_err_str(code); -1 for an unknown kind or bytes == NULL with len > 0. */
+int zp_reader_new(int kind, const uint8_t* bytes, uint64_t len, zp_reader_info* info);
+
+/* internet_checksum(data, accumulator) (checksum.rs:5-29): RFC 1071 sum of
+ * the big-endian 16-bit words (an odd tail byte as the high byte) with u32
+ * wrap-around, folded, complemented. */
+uint16_t zp_internet_checksum(const uint8_t* data, uint64_t len, uint32_t accumulator);
+/* verify_internet_checksum (checksum.rs:33-35): 1 if the checksum is 0. */
+int zp_verify_internet_checksum(const uint8_t* data, uint64_t len, uint32_t accumulator);
+/* pseudo_header(src, dest, protocol, length) (checksum.rs:38-69) for 4-byte
+ * (IPv4) or 16-byte (IPv6) addresses: the address words + protocol +
+ * (u32)length. addr_len other than 4 or 16 returns 0. */
+uint32_t zp_pseudo_header(const uint8_t* src, const uint8_t* dest, uint32_t addr_len,
+                          uint8_t protocol, uint64_t length);
 
 /* ------------------------------------------------------------------------- */
 /* Per-batch counters: frames per presence bit of          */

@@ -14,6 +14,15 @@
 // re-parsing (PacketParser::from_record). Errors are zp::Error carrying the
 // zp_err code and the exact reference string. Header-only; parse() and the
 // batch calls need libzp_hip.so (the GPU path), from_record() does not.
+//
+// The readers' checked constructors XReader::new(&[u8]) -> Result (the
+// reference's direct use, README.md:110-115) are XReader::create(Bytes),
+// which throws zp::Error on the reference's Err, and XReader::try_create
+// (Bytes, int* err), which returns std::nullopt and the code instead (`new`
+// is a C++ keyword). They go through zp_reader_new (libzp_hip.so; host
+// code, no device), as do zp::internet_checksum / verify_internet_checksum /
+// pseudo_header (checksum.rs:5,33,67). The explicit XReader(Bytes) view
+// constructors stay unchecked, as from_record needs them.
 #ifndef ZERO_PACKET_HPP
 #define ZERO_PACKET_HPP
 
@@ -64,13 +73,61 @@ template <size_t N> std::array<uint8_t, N> arr(Bytes b, size_t i) {
     return a;
 }
 [[noreturn]] inline void fail(int code) { throw Error(code, zp_err_string(code)); }
+
+// XReader::new through the C ABI: std::nullopt and *err on the reference's Err.
+template <class R>
+std::optional<R> try_new(Bytes b, int* err) {
+    zp_reader_info info;
+    const int rc = zp_reader_new(R::kKind, b.ptr, b.len, &info);
+    if (rc < 0) throw std::invalid_argument("zp_reader_new: null slice or unknown reader");
+    if (err) *err = rc;
+    if (rc != ZP_OK) return std::nullopt;
+    return R::from_info(b, info);
+}
+
+// The checked constructors every reader shares (CRTP): `create` throws
+// zp::Error with the reference's string, `try_create` returns std::nullopt.
+// A reader with more state than its slice (Ethernet, IPv6) has its own
+// from_info.
+template <class R, int K>
+struct Checked {
+    static constexpr int kKind = K;
+    static R from_info(Bytes b, const zp_reader_info&) { return R(b); }
+    static R create(Bytes b) {
+        int err = 0;
+        std::optional<R> r = try_new<R>(b, &err);
+        if (!r) fail(err);
+        return *r;
+    }
+    static std::optional<R> try_create(Bytes b, int* err = nullptr) { return try_new<R>(b, err); }
+};
 }  // namespace detail
 
+// checksum.rs:5-29 / :33-35 / :38-69 (the C ABI's host implementations).
+inline uint16_t internet_checksum(Bytes data, uint32_t accumulator) {
+    return zp_internet_checksum(data.ptr, data.len, accumulator);
+}
+inline bool verify_internet_checksum(Bytes data, uint32_t accumulator) {
+    return zp_verify_internet_checksum(data.ptr, data.len, accumulator) != 0;
+}
+inline uint32_t pseudo_header(const std::array<uint8_t, 4>& src, const std::array<uint8_t, 4>& dest,
+                              uint8_t protocol, size_t length) {
+    return zp_pseudo_header(src.data(), dest.data(), 4, protocol, length);
+}
+inline uint32_t pseudo_header(const std::array<uint8_t, 16>& src, const std::array<uint8_t, 16>& dest,
+                              uint8_t protocol, size_t length) {
+    return zp_pseudo_header(src.data(), dest.data(), 16, protocol, length);
+}
+
 // ethernet.rs:131-263
-class EthernetReader {
+class EthernetReader : public detail::Checked<EthernetReader, ZP_READER_ETHERNET> {
 public:
     Bytes bytes;
     EthernetReader(Bytes b, size_t header_len) : bytes(b), hl_(header_len) {}
+    // ethernet.rs:141-179: also the VLAN tagging checks
+    static EthernetReader from_info(Bytes b, const zp_reader_info& i) {
+        return EthernetReader(b, i.header_len);
+    }
     std::array<uint8_t, 6> dest_mac() const { return detail::arr<6>(bytes, 0); }
     std::array<uint8_t, 6> src_mac() const { return detail::arr<6>(bytes, 6); }
     uint16_t ethertype() const { return detail::be16(bytes, hl_ - 2); }
@@ -96,7 +153,7 @@ private:
 };
 
 // arp.rs:121-227
-class ArpReader {
+class ArpReader : public detail::Checked<ArpReader, ZP_READER_ARP> {
 public:
     Bytes bytes;
     explicit ArpReader(Bytes b) : bytes(b) {}
@@ -115,7 +172,7 @@ public:
 };
 
 // ipv4.rs:129-265
-class IPv4Reader {
+class IPv4Reader : public detail::Checked<IPv4Reader, ZP_READER_IPV4> {
 public:
     Bytes bytes;
     explicit IPv4Reader(Bytes b) : bytes(b) {}
@@ -135,6 +192,8 @@ public:
     size_t header_len() const { return (size_t)ihl() * 4; }
     Bytes header() const { check(); return bytes.sub(0, header_len()); }
     Bytes payload() const { check(); return bytes.sub(header_len()); }
+    // ipv4.rs:262-264: Err when header() is, else the header checksum
+    bool valid_checksum() const { return internet_checksum(header(), 0) == 0; }
 private:
     void check() const {   // ipv4.rs:238-241,252-255
         if (header_len() > bytes.size())
@@ -143,13 +202,17 @@ private:
 };
 
 // extensions/options.rs:76-154 (Hop-by-Hop, Destination Options)
-class OptionsHeaderReader {
+class OptionsHeaderReader : public detail::Checked<OptionsHeaderReader, ZP_READER_OPTIONS> {
 public:
     Bytes bytes;
     explicit OptionsHeaderReader(Bytes b) : bytes(b) {}
     uint8_t next_header() const { return bytes[0]; }
     uint8_t header_ext_len() const { return bytes[1]; }
     size_t header_len() const { return ((size_t)bytes[1] + 1) * 8; }
+    Bytes options() const {   // options.rs:111-119
+        if (bytes.size() < header_len()) detail::fail(ZP_ERR_OPTIONS_DATA_EXCEEDS);
+        return bytes.sub(2, header_len());
+    }
     Bytes header() const { check(); return bytes.sub(0, header_len()); }
     Bytes payload() const { check(); return bytes.sub(header_len()); }
 private:
@@ -160,7 +223,7 @@ private:
 };
 
 // extensions/routing.rs:99-195
-class RoutingHeaderReader {
+class RoutingHeaderReader : public detail::Checked<RoutingHeaderReader, ZP_READER_ROUTING> {
 public:
     Bytes bytes;
     explicit RoutingHeaderReader(Bytes b) : bytes(b) {}
@@ -168,6 +231,12 @@ public:
     uint8_t header_ext_len() const { return bytes[1]; }
     uint8_t routing_type() const { return bytes[2]; }
     uint8_t segments_left() const { return bytes[3]; }
+    // routing.rs:156-161 slices bytes[4..header_len] unchecked: the reference
+    // panics past the slice; this throws std::out_of_range there
+    Bytes data() const {
+        if (header_len() > bytes.size()) throw std::out_of_range("RoutingHeaderReader::data");
+        return bytes.sub(4, header_len());
+    }
     size_t header_len() const { return ((size_t)bytes[1] + 1) * 8; }
     Bytes header() const { check(); return bytes.sub(0, header_len()); }
     Bytes payload() const { check(); return bytes.sub(header_len()); }
@@ -179,7 +248,7 @@ private:
 };
 
 // extensions/fragment.rs:90-173
-class FragmentHeaderReader {
+class FragmentHeaderReader : public detail::Checked<FragmentHeaderReader, ZP_READER_FRAGMENT> {
 public:
     Bytes bytes;
     explicit FragmentHeaderReader(Bytes b) : bytes(b) {}
@@ -195,7 +264,8 @@ public:
 };
 
 // extensions/authentication.rs:97-200
-class AuthenticationHeaderReader {
+class AuthenticationHeaderReader
+    : public detail::Checked<AuthenticationHeaderReader, ZP_READER_AUTH> {
 public:
     Bytes bytes;
     explicit AuthenticationHeaderReader(Bytes b) : bytes(b) {}
@@ -205,6 +275,13 @@ public:
     uint32_t spi() const { return detail::be32(bytes, 4); }
     uint32_t sequence_number() const { return detail::be32(bytes, 8); }
     size_t header_len() const { return ((size_t)bytes[1] + 2) * 4; }
+    // authentication.rs:161-169; bytes[12..header_len] with header_len < 12
+    // (payload_len 0 or 1) panics in the reference: std::out_of_range here
+    Bytes authentication_data() const {
+        check();
+        if (header_len() < 12) throw std::out_of_range("AuthenticationHeaderReader::authentication_data");
+        return bytes.sub(12, header_len());
+    }
     Bytes header() const { check(); return bytes.sub(0, header_len()); }
     Bytes payload() const { check(); return bytes.sub(header_len()); }
 private:
@@ -226,13 +303,42 @@ struct ExtensionHeaders {
     uint8_t final_next_header = 0;
 };
 
+namespace detail {
+// A chain from its slot bits (flags >> shift) and zp_ext_offsets entries;
+// the offsets are relative to the IPv6 payload at frame[payload_off..].
+inline ExtensionHeaders ext_headers(Bytes frame, size_t payload_off, uint32_t flags, int shift,
+                                    const uint16_t* off, size_t total, uint8_t final_nh) {
+    ExtensionHeaders eh;
+    auto at = [&](int k) { return frame.sub(payload_off + off[k]); };
+    if (flags & (1u << (shift + ZP_EXT_HBH))) eh.hop_by_hop.emplace(at(ZP_EXT_HBH));
+    if (flags & (1u << (shift + ZP_EXT_RT))) eh.routing.emplace(at(ZP_EXT_RT));
+    if (flags & (1u << (shift + ZP_EXT_FRAG))) eh.fragment.emplace(at(ZP_EXT_FRAG));
+    if (flags & (1u << (shift + ZP_EXT_AH))) eh.auth_header.emplace(at(ZP_EXT_AH));
+    if (flags & (1u << (shift + ZP_EXT_DST1))) eh.destination_1st.emplace(at(ZP_EXT_DST1));
+    if (flags & (1u << (shift + ZP_EXT_DST2))) eh.destination_2nd.emplace(at(ZP_EXT_DST2));
+    eh.total_headers_len = total;
+    eh.final_next_header = final_nh;
+    return eh;
+}
+}  // namespace detail
+
 // ipv6.rs:135-286
-class IPv6Reader {
+class IPv6Reader : public detail::Checked<IPv6Reader, ZP_READER_IPV6> {
 public:
     Bytes bytes;
     std::optional<ExtensionHeaders> extension_headers;
     size_t extension_headers_len = 0;
     explicit IPv6Reader(Bytes b) : bytes(b) {}
+    // ipv6.rs:147-167: the constructor runs the extension walk (ipv6.rs:159)
+    static IPv6Reader from_info(Bytes b, const zp_reader_info& i) {
+        IPv6Reader r(b);
+        if (i.flags & ZP_F_EXT) {
+            r.extension_headers = detail::ext_headers(b, 40, i.flags, 12, i.ext.off, i.ext.len,
+                                                      i.final_nh);
+            r.extension_headers_len = i.ext.len;
+        }
+        return r;
+    }
     uint8_t version() const { return bytes[0] >> 4; }
     uint8_t traffic_class() const { return (uint8_t)(((bytes[0] & 0x0F) << 4) | (bytes[1] >> 4)); }
     uint32_t flow_label() const {
@@ -253,7 +359,7 @@ public:
 };
 
 // tcp.rs:132-244
-class TcpReader {
+class TcpReader : public detail::Checked<TcpReader, ZP_READER_TCP> {
 public:
     Bytes bytes;
     explicit TcpReader(Bytes b) : bytes(b) {}
@@ -268,10 +374,16 @@ public:
     uint16_t checksum() const { return detail::be16(bytes, 16); }
     uint16_t urgent_pointer() const { return detail::be16(bytes, 18); }
     size_t header_len() const { return (size_t)data_offset() * 4; }
+    Bytes header() const { check(); return bytes.sub(0, header_len()); }   // tcp.rs:223-231
+    Bytes payload() const { check(); return bytes.sub(header_len()); }     // tcp.rs:235-243
+private:
+    void check() const {
+        if (header_len() > bytes.size()) detail::fail(ZP_ERR_TCP_HDR_EXCEEDS);
+    }
 };
 
 // udp.rs:94-154
-class UdpReader {
+class UdpReader : public detail::Checked<UdpReader, ZP_READER_UDP> {
 public:
     Bytes bytes;
     explicit UdpReader(Bytes b) : bytes(b) {}
@@ -296,8 +408,14 @@ public:
     Bytes header() const { return bytes.sub(0, 8); }
     Bytes payload() const { return bytes.sub(8); }
 };
-class Icmpv4Reader : public IcmpReader { using IcmpReader::IcmpReader; };
-class Icmpv6Reader : public IcmpReader { using IcmpReader::IcmpReader; };
+class Icmpv4Reader : public IcmpReader, public detail::Checked<Icmpv4Reader, ZP_READER_ICMPV4> {
+public:
+    using IcmpReader::IcmpReader;
+};
+class Icmpv6Reader : public IcmpReader, public detail::Checked<Icmpv6Reader, ZP_READER_ICMPV6> {
+public:
+    using IcmpReader::IcmpReader;
+};
 
 // misc.rs:6-9: IpInIp::Ipv4(IPv4Reader) | IpInIp::Ipv6(IPv6Reader)
 struct IpInIp {
@@ -336,8 +454,8 @@ struct PacketParser {
         if (r.flags & ZP_F_IPV6) {
             IPv6Reader v6(frame.sub(hl));
             if (r.flags & ZP_F_EXT) {
-                v6.extension_headers = ext(frame, hl + 40, r.flags, 12, outer->off, outer->len,
-                                           r.final_nh);
+                v6.extension_headers = detail::ext_headers(frame, hl + 40, r.flags, 12, outer->off,
+                                                           outer->len, r.final_nh);
                 v6.extension_headers_len = outer->len;
             }
             p.ipv6 = v6;
@@ -348,8 +466,9 @@ struct PacketParser {
                 ii.kind = IpInIp::Kind::Ipv6;
                 IPv6Reader v6(frame.sub(r.inner_off));
                 if (r.flags & ZP_F_INNER_EXT) {
-                    v6.extension_headers = ext(frame, r.inner_off + 40, r.flags, 18, inner->off,
-                                               inner->len, r.inner_final_nh);
+                    v6.extension_headers = detail::ext_headers(frame, r.inner_off + 40, r.flags, 18,
+                                                               inner->off, inner->len,
+                                                               r.inner_final_nh);
                     v6.extension_headers_len = inner->len;
                 }
                 ii.ipv6 = v6;
@@ -378,22 +497,6 @@ struct PacketParser {
         if (rc < 0) throw std::runtime_error(std::string("zp_parse_one: ") + zp_last_error());
         if (ext_out) { ext_out[0] = e[0]; ext_out[1] = e[1]; }
         return from_record(frame, r, &e[0], &e[1]);
-    }
-
-private:
-    static ExtensionHeaders ext(Bytes frame, size_t payload_off, uint32_t flags, int shift,
-                                const uint16_t* off, size_t total, uint8_t final_nh) {
-        ExtensionHeaders eh;
-        auto at = [&](int k) { return frame.sub(payload_off + off[k]); };
-        if (flags & (1u << (shift + ZP_EXT_HBH))) eh.hop_by_hop.emplace(at(ZP_EXT_HBH));
-        if (flags & (1u << (shift + ZP_EXT_RT))) eh.routing.emplace(at(ZP_EXT_RT));
-        if (flags & (1u << (shift + ZP_EXT_FRAG))) eh.fragment.emplace(at(ZP_EXT_FRAG));
-        if (flags & (1u << (shift + ZP_EXT_AH))) eh.auth_header.emplace(at(ZP_EXT_AH));
-        if (flags & (1u << (shift + ZP_EXT_DST1))) eh.destination_1st.emplace(at(ZP_EXT_DST1));
-        if (flags & (1u << (shift + ZP_EXT_DST2))) eh.destination_2nd.emplace(at(ZP_EXT_DST2));
-        eh.total_headers_len = total;
-        eh.final_next_header = final_nh;
-        return eh;
     }
 };
 

@@ -45,6 +45,8 @@ static const char* const zp_err_strings[ZP_ERR_COUNT] = {
     "ICMPv6 type field is invalid.",
     "IPv4 encapsulated checksum is invalid.",
     "IPv6 encapsulated checksum is invalid.",
+    "Indicated TCP header length exceeds the allocated buffer.",
+    "Indicated header length exceeds the allocated buffer.",
 };
 
 static inline const char* zp_err_string(int code) {

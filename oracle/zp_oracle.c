@@ -413,6 +413,58 @@ int zpo_parse(const uint8_t* frame, size_t len, zp_record* rec, zp_ext_offsets* 
     return 0;
 }
 
+/* ---- standalone reader constructors (README.md:110-115) ------------------ */
+
+/* XReader::new(bytes) of reader `kind` (zp_reader_kind order). Returns 0 or
+ * the zp_err code; *hl = Ethernet header_len, and for IPv6 *flags = ZP_F_EXT
+ * + slot bits, *final_nh and *x the chain (zeros where absent). */
+int zpo_reader_new(int kind, const uint8_t* b, size_t n, uint32_t* hl, uint32_t* flags,
+                   uint8_t* final_nh, zp_ext_offsets* x) {
+    slice_t s = {b, n};
+    *hl = 0; *flags = 0; *final_nh = 0;
+    memset(x, 0, sizeof *x);
+    switch (kind) {
+    case 0:                                                     /* ethernet.rs:141-179 */
+        if (n < 14) return ZP_ERR_ETH_SLICE_TOO_SHORT;          /* :142-144 */
+        switch (be16(s, 12)) {
+        case 0x8100:
+            if (n < 18) return ZP_ERR_ETH_VLAN_TOO_SHORT;       /* :159-161 */
+            *hl = 18;
+            return 0;
+        case 0x88A8:
+            if (n < 22) return ZP_ERR_ETH_QINQ_TOO_SHORT;       /* :166-168 */
+            if (be16(s, 16) != 0x8100) return ZP_ERR_ETH_INVALID_QINQ;   /* :171-173 */
+            *hl = 22;
+            return 0;
+        default:
+            *hl = 14;
+            return 0;
+        }
+    case 1: return n < 28 ? ZP_ERR_ARP_TOO_SHORT : 0;           /* arp.rs:130-134 */
+    case 2: return n < 20 ? ZP_ERR_IPV4_TOO_SHORT : 0;          /* ipv4.rs:138-142 */
+    case 3: {                                                   /* ipv6.rs:147-167 */
+        ipv6_t r;
+        int err = ipv6_new(s, &r);
+        if (err) return err;
+        *final_nh = ipv6_final_nh(&r);
+        if (r.has_ext) {
+            *flags = ZP_F_EXT;
+            ext_to_record(&r, 12, flags, x);
+        }
+        return 0;
+    }
+    case 4: return n < 8 ? ZP_ERR_EXT_OPTIONS_TOO_SHORT : 0;    /* options.rs:83-87 */
+    case 5: return n < 8 ? ZP_ERR_EXT_ROUTING_TOO_SHORT : 0;    /* routing.rs:107-111 */
+    case 6: return n < 8 ? ZP_ERR_EXT_FRAGMENT_TOO_SHORT : 0;   /* fragment.rs:97-101 */
+    case 7: return n < 12 ? ZP_ERR_EXT_AUTH_TOO_SHORT : 0;      /* authentication.rs:105-109 */
+    case 8: return n < 20 ? ZP_ERR_TCP_TOO_SHORT : 0;           /* tcp.rs:141-145 */
+    case 9: return n < 8 ? ZP_ERR_UDP_TOO_SHORT : 0;            /* udp.rs:103-107 */
+    case 10: return n < 8 ? ZP_ERR_ICMP_TOO_SHORT : 0;          /* icmpv4.rs:92-96 */
+    case 11: return n < 8 ? ZP_ERR_ICMP_TOO_SHORT : 0;          /* icmpv6.rs:89-93 */
+    }
+    return -1;
+}
+
 /* ---- batch driver (CPU baseline) ----------------------------------------- */
 
 typedef struct {

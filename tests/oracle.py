@@ -60,6 +60,29 @@ def record_tuple(rec, ext):
             int(ext[1]["len"]), tuple(int(x) for x in ext[1]["off"]))
 
 
+def reader_new(kind, data):
+    """zpo_reader_new: XReader::new of reader `kind` (zp_reader_kind) ->
+    (err, header_len, ext flags, final_nh, ext EXT_DTYPE entry)."""
+    data = bytes(data)
+    buf = ctypes.create_string_buffer(data, max(len(data), 1))
+    return reader_new_at(ctypes.addressof(buf), len(data), kind)
+
+
+def reader_new_at(ptr, n, kind):
+    l = lib()
+    if not hasattr(l, "_rn_sig"):
+        l.zpo_reader_new.restype = ctypes.c_int
+        l.zpo_reader_new.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
+                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                     ctypes.c_void_p]
+        l._rn_sig = True
+    hl, fl, fnh = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint8()
+    x = np.zeros(1, EXT_DTYPE)
+    err = l.zpo_reader_new(kind, ptr, n, ctypes.byref(hl), ctypes.byref(fl), ctypes.byref(fnh),
+                           x.ctypes.data)
+    return err, hl.value, fl.value, fnh.value, x[0]
+
+
 def parse_batch(arena, offs, lens, nthreads=0):
     arena = np.ascontiguousarray(arena, dtype=np.uint8)
     offs = np.ascontiguousarray(offs).astype(np.uint64, copy=False)

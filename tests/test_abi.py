@@ -50,12 +50,12 @@ def test_err_strings(zp):
         35: "IPv6 encapsulated checksum is invalid.",
     }
     lib = zp._lib.hip()
-    assert lib.zp_abi_version() == 2
+    assert lib.zp_abi_version() == 3
     assert lib.zp_err_str(0) == b""
     for code, s in want.items():
         assert lib.zp_err_str(code).decode() == s
-    assert lib.zp_err_str(36) is None and lib.zp_err_str(-1) is None
-    for code in range(36):
+    assert lib.zp_err_str(38) is None and lib.zp_err_str(-1) is None
+    for code in range(38):
         assert lib.zp_err_str(code) is not None
 
 

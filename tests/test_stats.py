@@ -16,20 +16,20 @@ def expected(rec):
     """The counters from oracle records (numpy): flag bits, then err codes."""
     flags = rec["flags"].astype(np.uint64)
     out = [int(((flags >> np.uint64(b)) & np.uint64(1)).sum()) for b in range(24)]
-    out += list(np.bincount(rec["err"], minlength=36)[:36].astype(int))
+    out += list(np.bincount(rec["err"], minlength=38)[:38].astype(int))
     return np.array(out, np.int64)
 
 
 def test_names_match_header(zp):
     h = open(os.path.join(ROOT, "include", "zero_packet.h")).read()
     assert int(re.search(r"#define ZP_STATS_FLAG_BITS (\d+)", h).group(1)) == zp.stats.FLAG_BITS
-    assert zp.stats.COUNT == zp.stats.FLAG_BITS + len(zp.records.ERR_NAMES) == 60
+    assert zp.stats.COUNT == zp.stats.FLAG_BITS + len(zp.records.ERR_NAMES) == 62
     assert zp.stats.NAMES[6] == "tcp" and zp.stats.NAMES[12] == "ext:hop_by_hop"
-    assert zp.stats.NAMES[24] == "err:OK" and zp.stats.NAMES[-1] == "err:IPV6_L4_CHECKSUM"
+    assert zp.stats.NAMES[24] == "err:OK" and zp.stats.NAMES[-1] == "err:OPTIONS_DATA_EXCEEDS"
 
 
 def test_combine_sums_ranks(zp):
-    a, b = np.arange(60), np.ones(60, np.int64)
+    a, b = np.arange(62), np.ones(62, np.int64)
     assert (zp.stats.combine([a, b]) == a + 1).all()
 
 
@@ -81,7 +81,7 @@ def test_stats_byte_counter_flush(zp):
     got = zp.stats.count(recs).cpu().numpy()
     f = flags.cpu().numpy()
     want = [int(((f >> b) & 1).sum()) for b in range(24)]
-    want += list(np.bincount(err.cpu().numpy(), minlength=36).astype(int))
+    want += list(np.bincount(err.cpu().numpy(), minlength=38).astype(int))
     assert (got == np.array(want, np.int64)).all()
     assert got[0] > 40_000_000          # past the 8-bit range of one lane's byte counter
 

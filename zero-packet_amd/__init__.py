@@ -11,12 +11,15 @@ Import with importlib (the directory name has a hyphen):
   zp.builder.Chain / BuildBatch              batched PacketBuilder chains on the GPU
   zp.PacketParser.parse(frame)               one frame through the GPU path
   zp.PacketParser.from_record(frame, rec)    reference-shaped views over a record
+  zp.TcpReader.new(slice) ...                the readers' checked constructors (host)
+  zp.internet_checksum / pseudo_header       checksum.rs primitives (host)
 """
 from . import _lib, debugfmt, records, ring, shard  # noqa: F401
 from .parser import (ArpReader, AuthenticationHeaderReader, EthernetReader,  # noqa: F401
                      ExtensionHeaders, FragmentHeaderReader, Icmpv4Reader, Icmpv6Reader,
                      IpInIp, IPv4Reader, IPv6Reader, OptionsHeaderReader, PacketParser,
-                     RoutingHeaderReader, TcpReader, UdpReader, ZeroPacketError)
+                     RoutingHeaderReader, TcpReader, UdpReader, ZeroPacketError,
+                     internet_checksum, pseudo_header, verify_internet_checksum)
 
 try:  # torch-dependent batch API
     from . import batch, builder, columns, stats  # noqa: F401

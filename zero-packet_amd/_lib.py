@@ -50,6 +50,10 @@ def hip():
         _sig(lib, "zp_stats_device", i32, [vp, u64, vp, vp])
         _sig(lib, "zp_gen_lengths_device", i32, [i32, u64, u64, u64, vp, vp])
         _sig(lib, "zp_gen_frames_device", i32, [i32, u64, u64, u64, vp, vp, vp, vp])
+        _sig(lib, "zp_reader_new", i32, [i32, vp, u64, vp])
+        _sig(lib, "zp_internet_checksum", ctypes.c_uint16, [vp, u64, u32])
+        _sig(lib, "zp_verify_internet_checksum", i32, [vp, u64, u32])
+        _sig(lib, "zp_pseudo_header", u32, [vp, vp, u32, ctypes.c_uint8, u64])
         _hip = lib
     return _hip
 

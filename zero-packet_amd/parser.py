@@ -9,6 +9,15 @@ a record without re-parsing (PacketParser.from_record).
 
 PacketParser.parse(frame) parses through the GPU (zp_parse_one); batches go
 through zero-packet_amd.batch. There is no CPU parse path in this package.
+
+The reference's direct reader use (README.md:110-115), `TcpReader::new(&pkt)?`,
+is `TcpReader.new(pkt)`: the checked constructor of each reader, through
+zp_reader_new (host code of libzp_hip.so; Ethernet also checks its VLAN
+tagging, IPv6 runs the extension walk, ipv6.rs:159). It raises
+ZeroPacketError with the reference's string. `XReader(bytes)` stays the
+unchecked view that from_record builds. internet_checksum,
+verify_internet_checksum and pseudo_header are checksum.rs:5,33,67 through
+the same library.
 """
 import ctypes
 import threading
@@ -16,9 +25,10 @@ import threading
 import numpy as np
 
 from . import _lib
+from . import records as _rec
 from .records import (EXT_DTYPE, EXT_SLOTS, F_ARP, F_ETHERNET, F_EXT, F_EXT_SLOT, F_ICMPV4,
                       F_ICMPV6, F_INNER_EXT, F_INNER_EXT_SLOT, F_IP_IN_IP, F_IP_IN_IP_V6,
-                      F_IPV4, F_IPV6, F_TCP, F_UDP, RECORD_DTYPE)
+                      F_IPV4, F_IPV6, F_TCP, F_UDP, READER_INFO_DTYPE, RECORD_DTYPE)
 
 
 class ZeroPacketError(Exception):
@@ -37,34 +47,77 @@ def _be32(b, i):
     return (b[i] << 24) | (b[i + 1] << 16) | (b[i + 2] << 8) | b[i + 3]
 
 
-def _internet_checksum(data, acc=0):
-    s = acc & 0xFFFFFFFF
-    n = len(data) & ~1
-    for i in range(0, n, 2):
-        s = (s + ((data[i] << 8) | data[i + 1])) & 0xFFFFFFFF
-    if len(data) & 1:
-        s = (s + (data[-1] << 8)) & 0xFFFFFFFF
-    while s >> 16:
-        s = (s & 0xFFFF) + (s >> 16)
-    return (~s) & 0xFFFF
+def _buf(data):
+    data = bytes(data)
+    return data, ctypes.create_string_buffer(data, max(len(data), 1))
+
+
+def internet_checksum(data, accumulator=0):
+    """internet_checksum (checksum.rs:5-29) via zp_internet_checksum."""
+    data, b = _buf(data)
+    return int(_lib.hip().zp_internet_checksum(b, len(data), accumulator & 0xFFFFFFFF))
+
+
+def verify_internet_checksum(data, accumulator=0):
+    """verify_internet_checksum (checksum.rs:33-35)."""
+    data, b = _buf(data)
+    return bool(_lib.hip().zp_verify_internet_checksum(b, len(data), accumulator & 0xFFFFFFFF))
+
+
+def pseudo_header(src, dest, protocol, length):
+    """pseudo_header (checksum.rs:38-69) of 4-byte or 16-byte addresses."""
+    src, dest = bytes(src), bytes(dest)
+    if len(src) != len(dest) or len(src) not in (4, 16):
+        raise ValueError("pseudo_header: both addresses 4 bytes (IPv4) or 16 bytes (IPv6)")
+    return int(_lib.hip().zp_pseudo_header(src, dest, len(src), protocol & 0xFF, length))
+
+
+def _reader_new(kind, data):
+    """zp_reader_new: the reference constructor's checks; raises its Err."""
+    data, b = _buf(data)
+    info = np.zeros(1, READER_INFO_DTYPE)
+    rc = _lib.hip().zp_reader_new(kind, b, len(data), info.ctypes.data)
+    if rc < 0:
+        raise ValueError(f"zp_reader_new: bad arguments (kind {kind})")
+    if rc:
+        raise ZeroPacketError(_lib.hip().zp_err_str(rc).decode(), rc)
+    return data, info[0]
 
 
 class _Reader:
+    KIND = None
+
     def __init__(self, data):
         self.bytes = bytes(data)
 
     def __eq__(self, other):
         return type(self) is type(other) and self.bytes == other.bytes
 
+    @classmethod
+    def new(cls, data):
+        """XReader::new(&[u8]) -> Result: the checked constructor."""
+        data, info = _reader_new(cls.KIND, data)
+        return cls._from_info(data, info)
+
+    @classmethod
+    def _from_info(cls, data, info):
+        return cls(data)
+
 
 class EthernetReader(_Reader):
-    """ethernet.rs:131-263."""
+    """ethernet.rs:131-263. EthernetReader(data, header_len) is the view;
+    EthernetReader.new(data) (or header_len=None) the checked constructor."""
+    KIND = _rec.READER_ETHERNET
 
     def __init__(self, data, header_len=None):
         super().__init__(data)
-        if len(self.bytes) < 14:
-            raise ZeroPacketError("Slice is too short to contain an Ethernet frame.", 2)
-        self._hl = header_len if header_len is not None else self.calculate_header_len(self.bytes)
+        if header_len is None:
+            header_len = int(_reader_new(self.KIND, self.bytes)[1]["header_len"])
+        self._hl = header_len
+
+    @classmethod
+    def _from_info(cls, data, info):
+        return cls(data, int(info["header_len"]))
 
     @staticmethod
     def calculate_header_len(b):
@@ -121,6 +174,7 @@ class EthernetReader(_Reader):
 
 class ArpReader(_Reader):
     """arp.rs:121-227."""
+    KIND = _rec.READER_ARP
 
     def htype(self): return _be16(self.bytes, 0)
     def ptype(self): return _be16(self.bytes, 2)
@@ -138,6 +192,7 @@ class ArpReader(_Reader):
 
 class IPv4Reader(_Reader):
     """ipv4.rs:129-265."""
+    KIND = _rec.READER_IPV4
 
     def version(self): return self.bytes[0] >> 4
     def ihl(self): return self.bytes[0] & 0x0F
@@ -165,11 +220,13 @@ class IPv4Reader(_Reader):
         return self.bytes[self.header_len():]
 
     def valid_checksum(self):
-        return _internet_checksum(self.header(), 0) == 0
+        """ipv4.rs:262-264: raises when header() does."""
+        return internet_checksum(self.header(), 0) == 0
 
 
 class OptionsHeaderReader(_Reader):
     """extensions/options.rs:76-154 (Hop-by-Hop / Destination Options)."""
+    KIND = _rec.READER_OPTIONS
 
     def next_header(self): return self.bytes[0]
     def header_ext_len(self): return self.bytes[1]
@@ -177,7 +234,7 @@ class OptionsHeaderReader(_Reader):
 
     def options(self):
         if len(self.bytes) < self.header_len():
-            raise ZeroPacketError("Indicated header length exceeds the allocated buffer.")
+            raise ZeroPacketError("Indicated header length exceeds the allocated buffer.", 37)
         return self.bytes[2:self.header_len()]
 
     def header(self):
@@ -195,12 +252,18 @@ class OptionsHeaderReader(_Reader):
 
 class RoutingHeaderReader(_Reader):
     """extensions/routing.rs:99-195."""
+    KIND = _rec.READER_ROUTING
 
     def next_header(self): return self.bytes[0]
     def header_ext_len(self): return self.bytes[1]
     def routing_type(self): return self.bytes[2]
     def segments_left(self): return self.bytes[3]
-    def data(self): return self.bytes[4:self.header_len()]
+    def data(self):
+        """routing.rs:156-161 slices unchecked: the reference panics when the
+        header runs past the slice; IndexError here."""
+        if self.header_len() > len(self.bytes):
+            raise IndexError("RoutingHeaderReader.data: header past the slice")
+        return self.bytes[4:self.header_len()]
     def header_len(self): return (self.bytes[1] + 1) * 8
 
     def header(self):
@@ -218,6 +281,7 @@ class RoutingHeaderReader(_Reader):
 
 class FragmentHeaderReader(_Reader):
     """extensions/fragment.rs:90-173."""
+    KIND = _rec.READER_FRAGMENT
 
     def next_header(self): return self.bytes[0]
     def reserved(self): return self.bytes[1]
@@ -232,6 +296,7 @@ class FragmentHeaderReader(_Reader):
 
 class AuthenticationHeaderReader(_Reader):
     """extensions/authentication.rs:97-200."""
+    KIND = _rec.READER_AUTH
 
     def next_header(self): return self.bytes[0]
     def payload_len(self): return self.bytes[1]
@@ -241,9 +306,13 @@ class AuthenticationHeaderReader(_Reader):
     def header_len(self): return (self.bytes[1] + 2) * 4
 
     def authentication_data(self):
+        """authentication.rs:161-169; a header_len below 12 (payload_len 0 or
+        1) makes the reference's bytes[12..header_len] panic: IndexError."""
         if len(self.bytes) < self.header_len():
             raise ZeroPacketError(
                 "Indicated Authentication header length exceeds the allocated buffer.", 24)
+        if self.header_len() < 12:
+            raise IndexError("AuthenticationHeaderReader.authentication_data: header_len < 12")
         return self.bytes[12:self.header_len()]
 
     def header(self):
@@ -275,12 +344,23 @@ class ExtensionHeaders:
 
 class IPv6Reader(_Reader):
     """ipv6.rs:135-286. Built from a record: extension headers come from the
-    record's offsets instead of a re-walk."""
+    record's offsets instead of a re-walk. IPv6Reader.new(data) runs the walk
+    (ipv6.rs:147-167)."""
+    KIND = _rec.READER_IPV6
 
     def __init__(self, data, extension_headers=None, extension_headers_len=0):
         super().__init__(data)
         self.extension_headers = extension_headers
         self.extension_headers_len = extension_headers_len
+
+    @classmethod
+    def _from_info(cls, data, info):
+        flags = int(info["flags"])
+        if not flags & F_EXT:
+            return cls(data)
+        x = info["ext"]
+        eh = _ext_from(data, 40, flags, 12, x["off"], x["len"], info["final_nh"])
+        return cls(data, eh, int(x["len"]))
 
     def version(self): return self.bytes[0] >> 4
     def traffic_class(self): return ((self.bytes[0] & 0x0F) << 4) | (self.bytes[1] >> 4)
@@ -307,6 +387,7 @@ class IPv6Reader(_Reader):
 
 class TcpReader(_Reader):
     """tcp.rs:132-244."""
+    KIND = _rec.READER_TCP
 
     def src_port(self): return _be16(self.bytes, 0)
     def dest_port(self): return _be16(self.bytes, 2)
@@ -322,17 +403,18 @@ class TcpReader(_Reader):
 
     def header(self):
         if self.header_len() > len(self.bytes):
-            raise ZeroPacketError("Indicated TCP header length exceeds the allocated buffer.")
+            raise ZeroPacketError("Indicated TCP header length exceeds the allocated buffer.", 36)
         return self.bytes[:self.header_len()]
 
     def payload(self):
         if self.header_len() > len(self.bytes):
-            raise ZeroPacketError("Indicated TCP header length exceeds the allocated buffer.")
+            raise ZeroPacketError("Indicated TCP header length exceeds the allocated buffer.", 36)
         return self.bytes[self.header_len():]
 
 
 class UdpReader(_Reader):
     """udp.rs:94-154."""
+    KIND = _rec.READER_UDP
 
     def src_port(self): return _be16(self.bytes, 0)
     def dest_port(self): return _be16(self.bytes, 2)
@@ -354,10 +436,12 @@ class _IcmpReader(_Reader):
 
 class Icmpv4Reader(_IcmpReader):
     """icmpv4.rs:83-135."""
+    KIND = _rec.READER_ICMPV4
 
 
 class Icmpv6Reader(_IcmpReader):
     """icmpv6.rs:80-132."""
+    KIND = _rec.READER_ICMPV6
 
 
 class IpInIp:

@@ -12,6 +12,14 @@ assert RECORD_DTYPE.itemsize == 16
 EXT_DTYPE = np.dtype([("len", "<u2"), ("off", "<u2", (6,)), ("reserved", "<u2")])
 assert EXT_DTYPE.itemsize == 16
 RECORD_BYTES, EXT_BYTES = 16, 16
+# zp_reader_info (zp_reader_new): Ethernet header_len; IPv6 chain bits,
+# final_next_header and offsets.
+READER_INFO_DTYPE = np.dtype([("header_len", "<u4"), ("flags", "<u4"), ("final_nh", "u1"),
+                              ("reserved", "u1", (3,)), ("ext", EXT_DTYPE)])
+assert READER_INFO_DTYPE.itemsize == 28
+# zp_reader_kind
+(READER_ETHERNET, READER_ARP, READER_IPV4, READER_IPV6, READER_OPTIONS, READER_ROUTING,
+ READER_FRAGMENT, READER_AUTH, READER_TCP, READER_UDP, READER_ICMPV4, READER_ICMPV6) = range(12)
 
 
 def ext_match(got, want, rec):
@@ -51,5 +59,6 @@ ERR_NAMES = [
     "EXT_AUTH_TOO_SHORT", "EXT_AUTH_EXCEEDS", "TCP_TOO_SHORT", "TCP_DATA_OFFSET",
     "TCP_FLAGS", "UDP_TOO_SHORT", "UDP_LENGTH", "ICMP_TOO_SHORT", "ICMPV4_TYPE",
     "ICMPV4_CODE", "ICMPV6_TYPE", "IPV4_L4_CHECKSUM", "IPV6_L4_CHECKSUM",
+    "TCP_HDR_EXCEEDS", "OPTIONS_DATA_EXCEEDS",      # reader accessors only (ABI v3)
 ]
 ERR = {name: i for i, name in enumerate(ERR_NAMES)}
