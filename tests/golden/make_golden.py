@@ -17,7 +17,11 @@ What it writes, per fixture:
     the cited assert lines. `err` is only given where the test asserts
     is_err (or, for builder vectors the tests never parse, marked
     "derived": the first failing check of parser.rs for that frame).
-Also the checksum.rs:75-133 known-answer tests.
+Also the checksum.rs:75-133 known-answer tests, and the twelve per-reader
+`getters_and_setters` tests (ethernet.rs:285-310 ... icmpv6.rs:149-187) as
+`reader_getters`: the test buffer's length, every `writer.set_*` call with
+its value, and every `assert_eq!(reader.getter(), value)` with the expected
+value, the `let` bindings and length constants of the test resolved.
 """
 import json
 import os
@@ -53,6 +57,80 @@ def array_after(lines, lineno):
                 text.append(ch)
         i += 1
     raise ValueError(f"no array after line {lineno}")
+
+
+def _rust_value(expr, env):
+    """A literal of the getter tests: int (dec/hex), bool, [a, b, ..] or
+    [v; n], a `let` name or a constant, with & / .unwrap() stripped."""
+    e = expr.strip()
+    e = re.sub(r"\.unwrap\(\)$", "", e).lstrip("&").strip()
+    if e in env:
+        return env[e]
+    if e in ("true", "false"):
+        return e == "true"
+    m = re.fullmatch(r"\[(.+);\s*(\w+)\]", e, re.S)
+    if m:
+        return [_rust_value(m.group(1), env)] * _rust_value(m.group(2), env)
+    if e.startswith("["):
+        return [_rust_value(x, env) for x in e[1:-1].split(",") if x.strip()]
+    m = re.fullmatch(r"(0x[0-9a-fA-F_]+|\d[\d_]*)(?:u8|u16|u32|usize)?", e)
+    if m:
+        return int(m.group(1).replace("_", ""), 0)
+    raise ValueError(f"unparsed Rust value {expr!r}")
+
+
+def getter_tests(ref):
+    """The `getters_and_setters` test of each reader file, transcribed."""
+    files = [("ethernet", "src/datalink/ethernet.rs"), ("arp", "src/datalink/arp.rs"),
+             ("ipv4", "src/network/ipv4.rs"), ("ipv6", "src/network/ipv6.rs"),
+             ("options", "src/network/extensions/options.rs"),
+             ("routing", "src/network/extensions/routing.rs"),
+             ("fragment", "src/network/extensions/fragment.rs"),
+             ("authentication", "src/network/extensions/authentication.rs"),
+             ("tcp", "src/transport/tcp.rs"), ("udp", "src/transport/udp.rs"),
+             ("icmpv4", "src/network/icmpv4.rs"), ("icmpv6", "src/network/icmpv6.rs")]
+    out = []
+    for reader, rel in files:
+        lines = open(os.path.join(ref, rel)).read().splitlines()
+        env = {}
+        for ln in lines:                     # pub const X: usize = N;
+            m = re.match(r"\s*pub const (\w+): usize = (\d+);", ln)
+            if m:
+                env[m.group(1)] = int(m.group(2))
+        start = next(i for i, ln in enumerate(lines) if "fn getters_and_setters" in ln)
+        end = next(i for i in range(start + 1, len(lines)) if lines[i].rstrip() == "    }")
+        body = "\n".join(re.sub(r"//.*", "", ln) for ln in lines[start:end])
+        # statements end with ';' outside brackets (array literals and asserts
+        # span lines; `[0u8; 14]` holds one)
+        stmts, cur, depth = [], [], 0
+        for ch in body:
+            depth += (ch in "[(") - (ch in "])")
+            if ch == ";" and depth == 0:
+                stmts.append(" ".join("".join(cur).split()))
+                cur = []
+            else:
+                cur.append(ch)
+        buf, sets, asserts = None, [], []
+        for st in stmts:
+            m = re.match(r".*let mut bytes = \[0(?:u8)?; (\w+)\]", st)
+            if m:
+                buf = _rust_value(m.group(1), env)
+                continue
+            m = re.match(r".*let (\w+) = (.+)", st)
+            if m and "Writer::new" not in st and "Reader::new" not in st and "pseudo_header" not in st:
+                env[m.group(1)] = _rust_value(m.group(2), env)
+                continue
+            m = re.match(r".*writer\.set_(\w+)\((.*?)\)(?:\.unwrap\(\))?$", st)
+            if m:
+                arg = m.group(2).strip()
+                sets.append([m.group(1), None if arg in ("", "pseudo_sum") else _rust_value(arg, env)])
+                continue
+            m = re.match(r".*assert_eq!\( ?reader\.(\w+)\(\)(?:\.unwrap\(\))?, (.+?) ?\)$", st)
+            if m:
+                asserts.append([m.group(1), _rust_value(m.group(2), env)])
+        out.append({"reader": reader, "source": f"{rel}:{start}-{end + 1}",
+                    "buffer_len": buf, "sets": sets, "asserts": asserts})
+    return out
 
 
 def main(ref):
@@ -231,11 +309,12 @@ def main(ref):
     out = {"generated_by": "tests/golden/make_golden.py",
            "reference": "J-Schoepplenberg/zero-packet 0.1.0",
            "fixtures": fixtures, "builder_vectors": builder_vectors,
-           "checksum_kats": kats, "pseudo_header_kat": pseudo}
+           "checksum_kats": kats, "pseudo_header_kat": pseudo,
+           "reader_getters": getter_tests(ref)}
     with open(os.path.join(HERE, "parse_golden.json"), "w") as fh:
         json.dump(out, fh, indent=1)
     print(f"wrote {len(fixtures)} fixtures, {len(builder_vectors)} builder vectors, "
-          f"{len(kats)} checksum KATs")
+          f"{len(kats)} checksum KATs, {len(out['reader_getters'])} reader getter tests")
 
 
 if __name__ == "__main__":
