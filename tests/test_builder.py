@@ -458,3 +458,79 @@ def test_gpu_builder_descriptor_bounds_refused(zp):
         arena, torch.tensor([36], dtype=torch.int64, device=d),
         torch.tensor([64], dtype=torch.int32, device=d))
     assert int(res[0]["err"]) == 0 and int(arena[36 + 12].item()) == 0x08
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P,gap", [(200, 0), (200, 3), (1000, 0), (1000, 5)])
+def test_gpu_builder_payload_copies(zp, P, gap):
+    """set_payload(Some(..)) copies of P = 200 / 1000 bytes, each frame from
+    its own range of the data blob (the lane path copies past its window
+    straight from the blob; tcp.rs:108-114, udp.rs:82-88, builder.rs:473-474),
+    over IPv4 and IPv6 with every tagging, frames 0-300 B longer than the
+    chain, some too short (TCP_PAYLOAD / ICMPV4_PAYLOAD errors), random prior
+    contents; every arena byte, header_len and error identical to the oracle."""
+    import torch
+    rng = random.Random(P * 7 + gap)
+    C = zp.builder.Chain
+    chains, lens, fills = [], [], []
+    for k in range(2500):
+        tag = rng.randrange(3)
+        v6 = rng.random() < 0.3
+        et = 0x86DD if v6 else 0x0800
+        c = C()
+        if tag == 0:
+            c.ethernet(rb(rng, 6), rb(rng, 6), et); hl = 14
+        elif tag == 1:
+            c.ethernet_vlan(rb(rng, 6), rb(rng, 6), et, rng.randrange(65536)); hl = 18
+        else:
+            c.ethernet_qinq(rb(rng, 6), rb(rng, 6), et, rng.randrange(65536), rng.randrange(65536)); hl = 22
+        if v6:
+            c.ipv6(6, rng.randrange(256), rng.randrange(1 << 20), rng.randrange(65536), 17, 64,
+                   rb(rng, 16), rb(rng, 16))
+            hl += 40
+            addr = 16
+        else:
+            c.ipv4(4, 5, 0, 0, rng.randrange(65536), rng.randrange(65536), 0, 0, 64,
+                   rng.choice([6, 17, 1]), rb(rng, 4), rb(rng, 4))
+            hl += 20
+            addr = 4
+        pay = bytes(rb(rng, P - rng.randrange(0, 9)))        # ragged copy lengths
+        l4 = rng.choice(["tcp", "udp", "icmp"])
+        if l4 == "tcp":
+            c.tcp(rb(rng, addr), rng.randrange(65536), rb(rng, addr), rng.randrange(65536),
+                  rng.randrange(1 << 32), rng.randrange(1 << 32), 5, 0, 0x18, 65535, 0, pay)
+            hl += 20
+        elif l4 == "udp":
+            c.udp(rb(rng, addr), rng.randrange(65536), rb(rng, addr), rng.randrange(65536),
+                  rng.randrange(65536), pay)
+            hl += 8
+        elif v6:
+            c.icmpv6(rb(rng, 16), rb(rng, 16), 128, 0, pay)
+            hl += 8
+        else:
+            c.icmpv4(8, 0, pay)
+            hl += 8
+        size = hl + len(pay) + rng.randrange(0, 300) if rng.random() < 0.9 else \
+            hl + rng.randrange(0, len(pay))                  # payload does not fit
+        chains.append(c); lens.append(size)
+        fills.append(np.array(rb(rng, size), np.uint8))
+    before, want, offs, lens_, wres, packed = run_oracle(zp, chains, lens, fill=fills, align=3,
+                                                         gap=gap)
+    ops, op_start, data = packed
+    assert len(data) > 2000 * (P - 8)                         # one blob range per frame
+    d = torch.device("cuda:0")
+    arena = torch.from_numpy(before).to(d)
+    batch = zp.builder.BuildBatch()
+    for c in chains:
+        batch.add(c)
+    got = batch.run(arena, torch.from_numpy(offs.astype(np.int64)).to(d),
+                    torch.from_numpy(lens_.astype(np.int32)).to(d))
+    torch.cuda.synchronize()
+    ga = arena.cpu().numpy()
+    bad = [i for i, (o, l_) in enumerate(zip(offs, lens_))
+           if ga[o:o + l_].tobytes() != want[o:o + l_].tobytes()]
+    assert not bad, (len(bad), bad[:5], [int(wres[i]["err"]) for i in bad[:5]])
+    assert ga.tobytes() == want.tobytes()
+    assert got.tobytes() == wres.tobytes()
+    errs = {int(e) for e in wres["err"]}
+    assert 0 in errs and len(errs) >= 2, sorted(errs)

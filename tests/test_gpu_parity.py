@@ -590,3 +590,17 @@ def test_min_size_tiles_small_batches(zp):
     got, gext = gpu_parse(zp, a, same, l_[:64])
     assert_same(got, gext, want, wext)
     assert (want["err"] == 0).all()
+
+
+def test_config2_full_batch_exact(zp):
+    """BASELINE config 2 in full: the 1M x 64-B Eth+IPv4+UDP batch on the GPU,
+    byte-for-byte against the CPU oracle on the same frames (config 1)."""
+    import torch
+    arena, offs, lens = zp.batch.generate("c2", 1 << 20, device=dev())
+    recs, ext = zp.batch.parse_batch(arena, offs, lens)
+    torch.cuda.synchronize()
+    got, gext = zp.batch.records_to_numpy(recs, ext)
+    want, wext = orc.parse_batch(arena.cpu().numpy(), offs.cpu().numpy(), lens.cpu().numpy())
+    assert (want["err"] == 0).all() and (lens.cpu().numpy() == 64).all()
+    assert got.tobytes() == want.tobytes()
+    assert zp.records.ext_match(gext, wext, want)

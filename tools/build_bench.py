@@ -29,7 +29,11 @@ def main():
     ap.add_argument("--variants", default="", help="tools/variants/libzb_<name>.so builds to A/B")
     ap.add_argument("--payload", type=int, default=0,
                     help="copy min(P, room) payload bytes from the data blob into each frame "
-                         "(set_payload(Some(..)); chains past the lane window: the group pass)")
+                         "(set_payload(Some(..))); each frame from its own blob range")
+    ap.add_argument("--shared-blob", action="store_true",
+                    help="every frame copies from blob offset 0 (L2-resident source; round 2)")
+    ap.add_argument("--oracle-sample", type=int, default=2000,
+                    help="frames compared byte for byte with the oracle builder")
     args = ap.parse_args()
     zp = importlib.import_module("zero-packet_amd")
     B = zp.builder
@@ -76,14 +80,21 @@ def main():
     for o in (eth, ip, l4):
         o["data_len"] = B.NO_DATA
     pay = np.zeros(n, np.int64)
+    blob_bytes = 16
     if args.payload:
         start = np.where(tcp, 20, 8)
         pay = np.minimum(args.payload, ln - 34 - start)
         l4["data_len"] = pay.astype(np.uint32)
-        l4["data_off"] = 0
+        if args.shared_blob:
+            l4["data_off"] = 0
+            blob_bytes = max(16, args.payload)
+        else:                               # frame i copies blob[sum(pay[:i]) ...]: from HBM
+            l4["data_off"] = (np.cumsum(pay) - pay).astype(np.uint32)
+            blob_bytes = max(16, int(pay.sum()))
+            assert blob_bytes < (1 << 32)
     t_ops = torch.from_numpy(ops.view(np.uint8)).to(d)
     t_start = torch.arange(0, 3 * n + 1, 3, dtype=torch.int32, device=d)
-    t_data = torch.from_numpy(rng.integers(0, 256, max(16, args.payload), dtype=np.uint8)).to(d)
+    t_data = torch.randint(0, 256, (blob_bytes,), dtype=torch.uint8, device=d)
     res = torch.zeros((n, 8), dtype=torch.uint8, device=d)
     import ctypes
     libs = [("base", zp._lib.hip())]
@@ -95,6 +106,7 @@ def main():
         libs.append((v, l_))
     s = torch.cuda.current_stream(d)
     snapshot = arena.clone()
+    blob_read = int(pay.sum()) if args.payload and not args.shared_blob else 0
     errs = 0
     ref = None
     for name, lib in libs:
@@ -121,10 +133,36 @@ def main():
         nbytes = int(ln.sum())
         hdr = n * 54 + int(pay.sum())
         opb = int(t_ops.numel() + t_start.numel() * 4)
-        print(f"build c3 x {n}{f' payload {args.payload}' if args.payload else ''} [{name}]: {ms:.3f} ms  {n / ms / 1e3:.0f} Mpkt/s  "
-              f"{(nbytes + hdr) / ms / 1e6:.0f} GB/s (frame read + header write; "
-              f"{(nbytes + hdr + opb) / ms / 1e6:.0f} with the op reads)  errors {errs}",
-              flush=True)
+        alg = nbytes + hdr + blob_read
+        blob = " shared-blob" if args.shared_blob else ""
+        print(f"build c3 x {n}{f' payload {args.payload}{blob}' if args.payload else ''} [{name}]: "
+              f"{ms:.3f} ms  {n / ms / 1e3:.0f} Mpkt/s  "
+              f"{alg / ms / 1e6:.0f} GB/s = {alg / ms / 1e6 / 8000:.3f} of 8 TB/s (frame read "
+              f"{nbytes / 1e9:.2f} + header/payload write {hdr / 1e9:.2f} + blob read "
+              f"{blob_read / 1e9:.2f} GB; {(alg + opb) / ms / 1e6:.0f} GB/s with the op reads)  "
+              f"errors {errs}", flush=True)
+    if args.oracle_sample:
+        # a sample of the built frames against the oracle builder, from the
+        # same prior bytes, ops and blob ranges
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle as orc
+        idx = np.sort(rng.choice(n, min(n, args.oracle_sample), replace=False))
+        o_h, l_h = offs.cpu().numpy()[idx], ln[idx]
+        snap = snapshot.cpu().numpy()
+        blob = t_data.cpu().numpy()
+        a_s = np.zeros(int(l_h.sum()) + 64, np.uint8)
+        so = np.concatenate([[0], np.cumsum(l_h)[:-1]]).astype(np.uint64)
+        for k, (o, l_) in enumerate(zip(o_h, l_h)):
+            a_s[so[k]:so[k] + l_] = snap[o:o + l_]
+        ops_s = np.stack([eth[idx], ip[idx], l4[idx]], axis=1).reshape(-1).copy()
+        res_s = orc.build_batch(a_s, so, l_h.astype(np.uint32), ops_s,
+                                np.arange(0, 3 * len(idx) + 1, 3, dtype=np.uint32), blob)
+        got = ref.cpu().numpy()             # the first launch from the snapshot
+        bad = sum(1 for k, (o, l_) in enumerate(zip(o_h, l_h))
+                  if got[o:o + l_].tobytes() != a_s[so[k]:so[k] + l_].tobytes())
+        print(f"oracle sample: {len(idx) - bad}/{len(idx)} frames byte-identical, "
+              f"{int((res_s[:, 4] != 0).sum())} oracle errors", flush=True)
+        assert bad == 0
     recs, _ = zp.batch.parse_batch(arena, offs, lens)
     torch.cuda.synchronize()
     bad = int((recs[:, 4] != 0).sum())

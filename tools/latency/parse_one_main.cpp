@@ -1,0 +1,60 @@
+// Per-frame latency of zp_parse_one (PacketParser::parse for one frame,
+// parser.rs:53, through the GPU: H2D -> kernel -> D2H -> sync), the drop-in
+// for a caller that parses frame by frame. stdin: frame hex lines.
+//   parse_one_main <threads> <calls per thread>
+// Each thread owns one zp::Context (a zp_ctx may not be shared) and parses
+// the frames round robin; prints mean / p50 / p99 microseconds per call and
+// the aggregate calls per second.
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <iostream>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "zero_packet.hpp"
+
+int main(int argc, char** argv) {
+    const int threads = argc > 1 ? std::atoi(argv[1]) : 1;
+    const int calls = argc > 2 ? std::atoi(argv[2]) : 2000;
+    std::vector<std::vector<uint8_t>> frames;
+    std::string line;
+    while (std::getline(std::cin, line)) {
+        std::vector<uint8_t> v(line.size() / 2);
+        for (size_t i = 0; i < v.size(); ++i) v[i] = (uint8_t)std::stoul(line.substr(2 * i, 2), nullptr, 16);
+        frames.push_back(v);
+    }
+    std::vector<std::vector<double>> lat(threads);
+    std::vector<int> bad(threads, 0);
+    auto worker = [&](int t) {
+        zp::Context ctx(0);
+        for (int w = 0; w < 50; ++w) ctx.parse(zp::Bytes{frames[0].data(), frames[0].size()});
+        lat[t].reserve(calls);
+        for (int k = 0; k < calls; ++k) {
+            const auto& f = frames[(k + t) % frames.size()];
+            const auto t0 = std::chrono::steady_clock::now();
+            zp::PacketParser p = ctx.parse(zp::Bytes{f.data(), f.size()});
+            const auto t1 = std::chrono::steady_clock::now();
+            if (!p.ethernet) ++bad[t];
+            lat[t].push_back(std::chrono::duration<double, std::micro>(t1 - t0).count());
+        }
+    };
+    const auto t0 = std::chrono::steady_clock::now();
+    std::vector<std::thread> th;
+    for (int t = 0; t < threads; ++t) th.emplace_back(worker, t);
+    for (auto& x : th) x.join();
+    const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    std::vector<double> all;
+    for (auto& v : lat) all.insert(all.end(), v.begin(), v.end());
+    std::sort(all.begin(), all.end());
+    double sum = 0;
+    for (double x : all) sum += x;
+    int nbad = 0;
+    for (int b : bad) nbad += b;
+    std::printf("{\"threads\": %d, \"calls\": %zu, \"mean_us\": %.2f, \"p50_us\": %.2f, "
+                "\"p99_us\": %.2f, \"calls_per_s\": %.0f, \"rejected\": %d}\n",
+                threads, all.size(), sum / all.size(), all[all.size() / 2],
+                all[(size_t)(all.size() * 0.99)], all.size() / wall, nbad);
+    return nbad ? 1 : 0;
+}
