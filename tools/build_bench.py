@@ -153,13 +153,14 @@ def main():
         a_s = np.zeros(int(l_h.sum()) + 64, np.uint8)
         so = np.concatenate([[0], np.cumsum(l_h)[:-1]]).astype(np.uint64)
         for k, (o, l_) in enumerate(zip(o_h, l_h)):
-            a_s[so[k]:so[k] + l_] = snap[o:o + l_]
+            a_s[int(so[k]):int(so[k]) + int(l_)] = snap[int(o):int(o) + int(l_)]
         ops_s = np.stack([eth[idx], ip[idx], l4[idx]], axis=1).reshape(-1).copy()
         res_s = orc.build_batch(a_s, so, l_h.astype(np.uint32), ops_s,
                                 np.arange(0, 3 * len(idx) + 1, 3, dtype=np.uint32), blob)
         got = ref.cpu().numpy()             # the first launch from the snapshot
         bad = sum(1 for k, (o, l_) in enumerate(zip(o_h, l_h))
-                  if got[o:o + l_].tobytes() != a_s[so[k]:so[k] + l_].tobytes())
+                  if got[int(o):int(o) + int(l_)].tobytes() !=
+                  a_s[int(so[k]):int(so[k]) + int(l_)].tobytes())
         print(f"oracle sample: {len(idx) - bad}/{len(idx)} frames byte-identical, "
               f"{int((res_s[:, 4] != 0).sum())} oracle errors", flush=True)
         assert bad == 0

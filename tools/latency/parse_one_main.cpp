@@ -27,10 +27,12 @@ int main(int argc, char** argv) {
     }
     std::vector<std::vector<double>> lat(threads);
     std::vector<int> bad(threads, 0);
+    std::vector<double> busy(threads, 0);
     auto worker = [&](int t) {
         zp::Context ctx(0);
         for (int w = 0; w < 50; ++w) ctx.parse(zp::Bytes{frames[0].data(), frames[0].size()});
         lat[t].reserve(calls);
+        const auto tb = std::chrono::steady_clock::now();
         for (int k = 0; k < calls; ++k) {
             const auto& f = frames[(k + t) % frames.size()];
             const auto t0 = std::chrono::steady_clock::now();
@@ -39,12 +41,13 @@ int main(int argc, char** argv) {
             if (!p.ethernet) ++bad[t];
             lat[t].push_back(std::chrono::duration<double, std::micro>(t1 - t0).count());
         }
+        busy[t] = std::chrono::duration<double>(std::chrono::steady_clock::now() - tb).count();
     };
-    const auto t0 = std::chrono::steady_clock::now();
     std::vector<std::thread> th;
     for (int t = 0; t < threads; ++t) th.emplace_back(worker, t);
     for (auto& x : th) x.join();
-    const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    double wall = 0;             // the timed loops (context creation and warm-up excluded)
+    for (double b : busy) wall = b > wall ? b : wall;
     std::vector<double> all;
     for (auto& v : lat) all.insert(all.end(), v.begin(), v.end());
     std::sort(all.begin(), all.end());

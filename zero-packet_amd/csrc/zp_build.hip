@@ -687,16 +687,28 @@ __device__ __forceinline__ uint4 ld_region(const uint8_t ZB_LDSP* r, uint32_t at
 // W = V (segment starts at an odd address) or W == 256 V (mod 65535); the
 // fold of S = acc + W depends only on S mod 65535 and on S == 0 (exact for
 // frames up to 64 KiB, the only ones this path takes).
+// The folded checksum from V (arena parity, exact), the accumulator and the
+// parity of the segment's first byte.
+__device__ __forceinline__ uint16_t fold_v(uint32_t V, uint32_t acc, bool even) {
+    if (acc == 0 && V == 0) return 0xFFFF;                 // S == 0: !fold(0)
+    uint32_t w = V % 65535u;
+    if (even) w = (w * 256u) % 65535u;
+    const uint32_t r = (acc % 65535u + w) % 65535u;
+    return (uint16_t)~(r ? r : 65535u);
+}
+
 struct WinCsum {
     const uint8_t ZB_LDSP* region;    // the lane's window, from A & ~15
     uint4 tail;                       // the frame's last chunk (original bytes)
     uintptr_t ga;
     uint32_t shift, len, nchw, fsum;
-    uint32_t pdelta;                  // V change of a payload copied past the window
     uint32_t vorig[ZP_WIN_CH];
+    // what csum() saw, for a payload copied past the window after the chain
+    // (coop_payload): the checksum is then refolded with the copy's V change
+    mutable uint32_t cs_V, cs_acc, cs_l4;
     __device__ uint16_t csum(uint32_t l4, uint32_t acc) const {
         const uint32_t y4 = l4 + shift, c4 = y4 >> 4;
-        uint32_t vall = fsum + pdelta, before = 0;
+        uint32_t vall = fsum, before = 0;
 #pragma unroll
         for (uint32_t c = 0; c < ZP_WIN_CH; ++c) {
             if (c < nchw) {
@@ -710,11 +722,8 @@ struct WinCsum {
         const uint32_t he = (len + shift) & 15u;
         const uint32_t ex = he ? range_sum(tail, he, 16u) : 0u;
         const uint32_t V = vall - before - ex;
-        if (acc == 0 && V == 0) return 0xFFFF;             // S == 0: !fold(0)
-        uint32_t w = V % 65535u;
-        if (!((ga + l4) & 1)) w = (w * 256u) % 65535u;
-        const uint32_t r = (acc % 65535u + w) % 65535u;
-        return (uint16_t)~(r ? r : 65535u);
+        cs_V = V; cs_acc = acc; cs_l4 = l4;
+        return fold_v(V, acc, !((ga + l4) & 1));
     }
 };
 
@@ -771,60 +780,135 @@ __device__ __forceinline__ uint32_t chain_extent(const OpGlobal& ops, uint32_t n
 #define ZB_LANE_PAY 1          // payload copies past the window on the lane path
 #endif
 
-// V (little-endian words at even ARENA addresses) and the plain byte sum B of
-// global bytes [a0, a1): aligned dword loads, ZB_PAY_DW in flight.
-#ifndef ZB_PAY_DW
-#define ZB_PAY_DW 8
+// Wave-cooperative segments: lane j owns cnt_j chunks; the wave walks the
+// concatenation of all lanes' chunks in items of 64 (lane l of item i takes
+// virtual chunk 64 i + l, its owner j found by a binary search over the
+// owners' exclusive prefix with ds_bpermute), ZB_COOP_U items at a time:
+// load(j, k, live) issues chunk k of owner j's loads for all of them first,
+// then use(data, j, k, live) consumes them (stores, a u32 contribution), so
+// ZB_COOP_U items' loads are in flight per wave. Returns, per lane, the
+// wrapping sum of its own chunks' contributions (running-sum differences:
+// no segmented reduction). Every lane must be active (DPP scans, bpermute).
+#ifndef ZB_COOP_U
+#define ZB_COOP_U 2            // 1: 2.04 / 3.52 ms, 2: 1.95 / 3.16, 4: 1.99 / 3.26, 8: 2.11 / 3.52 (P = 200 / 1000)
 #endif
-__device__ __forceinline__ void gsum_vb(uintptr_t a0, uintptr_t a1, uint32_t& V, uint32_t& B) {
-    V = 0;
-    B = 0;
-    const uintptr_t d0 = a0 & ~(uintptr_t)3;
-    for (uintptr_t d = d0; d < a1; d += 4 * ZB_PAY_DW) {
-        uint32_t x[ZB_PAY_DW];
+template <class D, class L, class U>
+__device__ __forceinline__ uint32_t wave_segments(uint32_t cnt, int lane, L&& load, U&& use) {
+    const uint32_t incl = wave_scan(cnt), pre = incl - cnt;
+    const uint32_t T = rdl(incl, 63);
+    uint32_t carry = 0, p_pre = 0, p_end = 0;
+    for (uint32_t base = 0; base < T; base += 64 * ZB_COOP_U) {
+        uint32_t jj[ZB_COOP_U], kk[ZB_COOP_U];
+        D d[ZB_COOP_U];
 #pragma unroll
-        for (int u = 0; u < ZB_PAY_DW; ++u) {
-            const uintptr_t a = d + 4u * u;
-            x[u] = a < a1 ? *(const ZP_GLOBAL uint32_t*)a : 0u;
+        for (int u = 0; u < ZB_COOP_U; ++u) {
+            const uint32_t g = base + 64u * u + (uint32_t)lane;
+            uint32_t j = 0;                              // largest j with pre_j <= g
+#pragma unroll
+            for (uint32_t st = 32; st; st >>= 1)
+                j = bperm(pre, j + st) <= g ? j + st : j;
+            jj[u] = j;
+            kk[u] = g - bperm(pre, j);
+            d[u] = load(j, kk[u], g < T);
         }
 #pragma unroll
-        for (int u = 0; u < ZB_PAY_DW; ++u) {
-            const uintptr_t a = d + 4u * u;
-            if (a < a1) {
-                const int lo = a0 > a ? (int)(a0 - a) : 0;
-                const int hi = a1 - a < 4 ? (int)(a1 - a) : 4;
-                const uint32_t m = x[u] & byte_mask(0, lo, hi);
-                V = sad16(m, V);
-                B = __builtin_amdgcn_sad_u8(m, 0u, B);
-            }
+        for (int u = 0; u < ZB_COOP_U; ++u) {
+            const uint32_t b = base + 64u * u;
+            const uint32_t v = use(d[u], jj[u], kk[u], b + (uint32_t)lane < T);
+            const uint32_t inc = wave_scan(v), exc = inc - v;
+            const uint32_t xp = bperm(exc, (pre - b) & 63u), xe = bperm(exc, (incl - b) & 63u);
+            if (pre >= b && pre < b + 64) p_pre = carry + xp;
+            if (incl >= b && incl < b + 64) p_end = carry + xe;
+            carry += rdl(inc, 63);
         }
     }
+    if (pre >= T) p_pre = carry;
+    if (incl >= T) p_end = carry;
+    return p_end - p_pre;
 }
 
-// Copies global bytes [src, src + n) to [dst, dst + n) (n < 64 KiB, no
-// overlap): byte stores up to a 4-aligned destination, then 4 ZB_PAY_DW bytes
-// per trip from aligned source dwords, then byte stores.
-__device__ __forceinline__ void gcopy(uintptr_t dst, uintptr_t src, uint32_t n) {
-    uint32_t q = 0;
-    for (; q < n && ((dst + q) & 3); ++q)
-        *(ZP_GLOBAL uint8_t*)(dst + q) = *(const ZP_GLOBAL uint8_t*)(src + q);
-    const uintptr_t send = src + n;
-    for (; q + 4 * ZB_PAY_DW <= n; q += 4 * ZB_PAY_DW) {
-        const uintptr_t s0 = src + q, sb = s0 & ~(uintptr_t)3;
-        const uint32_t sh = (uint32_t)(s0 & 3);
-        uint32_t x[ZB_PAY_DW + 1];
-#pragma unroll
-        for (int k = 0; k <= ZB_PAY_DW; ++k) {
-            const uintptr_t a = sb + 4u * k;
-            x[k] = (k < ZB_PAY_DW || (sh && a < send)) ? *(const ZP_GLOBAL uint32_t*)a : 0u;
-        }
-#pragma unroll
-        for (int k = 0; k < ZB_PAY_DW; ++k)
-            *(ZP_GLOBAL uint32_t*)(dst + q + 4u * k) = __builtin_amdgcn_alignbyte(x[k + 1], x[k], sh);
-    }
-    for (; q < n; ++q)
-        *(ZP_GLOBAL uint8_t*)(dst + q) = *(const ZP_GLOBAL uint8_t*)(src + q);
+__device__ __forceinline__ uint64_t bperm64(uint64_t v, uint32_t r) {
+    return ((uint64_t)bperm((uint32_t)(v >> 32), r) << 32) | bperm((uint32_t)v, r);
 }
+
+struct CopyChunk { uint32_t x[5]; uintptr_t X; uint32_t m, sh; };
+struct SumChunk { uint4 q; uint32_t l, h, neg; };
+
+// The payload bytes past the window, for every lane whose chain copied a
+// payload that reaches past it (go): destination [D0, D1) of its frame
+// (D0 = the window end, 16-B aligned), from the blob at src. The whole wave
+// moves 16-B chunks: coalesced loads of the blob, full 16-B stores (the last
+// chunk of a copy byte by byte), each blob and frame byte touched once.
+// Returns the copy's change of the frame's V (arena parity): V of the copied
+// bytes at their destination minus V of the bytes they replace. The latter
+// is summed over the shorter of two ranges of original bytes, read before
+// any copy is written (a first pass): [D0, D1) itself (kind A), or the
+// frame's bytes after the copy [D1, FE) (kind B), then V(D0, D1) = the
+// frame's stream sum - its window chunks - V(D1, FE) - the bytes past its
+// end in its last chunk (cB, from the kept original chunk: in HBM they are
+// the next frame's, whose lane may be rewriting them).
+__device__ __forceinline__ uint32_t coop_payload(bool go, uintptr_t D0, uintptr_t D1, uintptr_t FE,
+                                                 uintptr_t src, uint32_t cB, int lane) {
+    const uint32_t mc = go ? (uint32_t)(D1 - D0) : 0u;
+    const bool kA = mc <= (uint32_t)(FE - D1);
+    const uintptr_t R0 = kA ? D0 : (D1 & ~(uintptr_t)15);
+    const uint32_t rlo = go ? (uint32_t)((kA ? D0 : D1) - R0) : 0u;
+    const uint32_t rhi = go ? (uint32_t)((kA ? D1 : FE) - R0) : 0u;
+    // pass 1: original bytes (loads only)
+    const uint32_t vo = wave_segments<SumChunk>(
+        (rhi + 15) >> 4, lane,
+        [&](uint32_t j, uint32_t k, bool live) {
+            const uintptr_t r0 = bperm64(R0, j);
+            SumChunk c;
+            const uint32_t lo = bperm(rlo, j), hi = bperm(rhi, j);
+            c.neg = bperm(kA ? 1u : 0u, j);
+            const uint32_t a = 16u * k;
+            c.l = lo > a ? lo - a : 0u;
+            c.h = hi - a < 16u ? hi - a : 16u;
+            c.q = live ? ldg16(r0 + a) : make_uint4(0, 0, 0, 0);
+            return c;
+        },
+        [&](const SumChunk& c, uint32_t, uint32_t, bool live) {
+            if (!live) return 0u;
+            const uint32_t v = range_sum(c.q, c.l, c.h);
+            return c.neg ? 0u - v : v;
+        });
+    // pass 2: the copy
+    const uint32_t vn = wave_segments<CopyChunk>(
+        (mc + 15) >> 4, lane,
+        [&](uint32_t j, uint32_t k, bool live) {
+            const uintptr_t d0 = bperm64(D0, j), s0 = bperm64(src, j);
+            const uint32_t m_all = bperm(mc, j);
+            CopyChunk c;
+            c.m = m_all - 16u * k < 16u ? m_all - 16u * k : 16u;
+            const uintptr_t S = s0 + 16u * k, sb = S & ~(uintptr_t)3, send = S + c.m;
+            c.sh = (uint32_t)(S & 3);
+            c.X = d0 + 16u * k;
+#pragma unroll
+            for (int u = 0; u < 5; ++u) {
+                const uintptr_t a = sb + 4u * u;
+                c.x[u] = live && a < send ? *(const ZP_GLOBAL uint32_t*)a : 0u;
+            }
+            return c;
+        },
+        [&](const CopyChunk& c, uint32_t, uint32_t, bool live) {
+            if (!live) return 0u;
+            const uint4 q = make_uint4(__builtin_amdgcn_alignbyte(c.x[1], c.x[0], c.sh),
+                                       __builtin_amdgcn_alignbyte(c.x[2], c.x[1], c.sh),
+                                       __builtin_amdgcn_alignbyte(c.x[3], c.x[2], c.sh),
+                                       __builtin_amdgcn_alignbyte(c.x[4], c.x[3], c.sh));
+            if (c.m == 16) {
+                *(ZP_GLOBAL zp_u32x4*)c.X = zp_u32x4{q.x, q.y, q.z, q.w};
+            } else {
+                const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+                for (uint32_t b = 0; b < c.m; ++b)
+                    *(ZP_GLOBAL uint8_t*)(c.X + b) = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
+            }
+            return range_sum(q, 0, c.m);
+        });
+    return vn + (go && !kA ? cB + vo : vo);
+}
+
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZB_FAST_WPE)))
 zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs,
                      const uint32_t* __restrict__ lens, uint64_t n,
@@ -904,7 +988,6 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
         wc.nchw = nch < ZP_WIN_CH ? nch : ZP_WIN_CH;
         wc.fsum = lds.cend[s.rank] - (s.rank ? lds.cend[s.rank - 1] : 0u);
         wc.tail = tail[rank];
-        wc.pdelta = 0;
         ptail = tail[(rank - 1) & 63u];
 #pragma unroll
         for (uint32_t c = 0; c < ZP_WIN_CH; ++c) {
@@ -925,47 +1008,42 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
         wc.region = region;
         BView<uint8_t ZB_LDSP*> v{region + s.shift, len, true};
 #if ZB_LANE_PAY
-        if (pay) {
-            v.lim = s.wlen;
-            // The L4 checksum sees the payload bytes past the window in place
-            // of the frame's: V(blob part, at its destination's parity) -
-            // V(original bytes). A copy that does not fit the frame fails in
-            // the chain before any byte is written; nothing to add then.
-            const uint32_t q0 = s.wlen > pay_at ? s.wlen : pay_at, pe = pay_at + pay_len;
-            if (pe <= len) {
-                const uintptr_t src = (uintptr_t)data + og.get(nops - 1).data_off + (q0 - pay_at);
-                // V of the original bytes [q0, pe): read where that is
-                // shorter than the rest of the frame; otherwise the stream's
-                // sum of the frame's chunks minus the window's chunks, the
-                // frame's bytes between the window and q0 and from pe to its
-                // end, and the bytes past its end in its last chunk, from the
-                // kept original chunk (in HBM they are the next frame's, which
-                // its lane may be rewriting). Only this lane writes [q0, pe),
-                // and only after the chain.
-                uint32_t Vo, Bo, Vb, Bb;
-                if (pe - q0 <= len - pe) {
-                    gsum_vb(s.ga + q0, s.ga + pe, Vo, Bo);
-                } else {
-                    uint32_t Vw = 0;
-#pragma unroll
-                    for (uint32_t c = 0; c < ZP_WIN_CH; ++c) Vw += wc.vorig[c];
-                    const uint32_t he = (len + s.shift) & 15u;
-                    uint32_t Vh, Bh, Vt, Bt;
-                    gsum_vb(s.ga + s.wlen, s.ga + q0, Vh, Bh);
-                    gsum_vb(s.ga + pe, s.ga + len, Vt, Bt);
-                    const uint32_t Vx = he ? range_sum(wc.tail, he, 16u) : 0u;
-                    Vo = wc.fsum - Vw - Vh - Vt - Vx;
-                }
-                gsum_vb(src, src + (pe - q0), Vb, Bb);
-                const uint32_t O = (Vb - Bb) / 255u, E = Bb - O;   // blob bytes at odd / even addresses
-                const uint32_t Vd = ((src ^ (s.ga + q0)) & 1) ? O + 256u * E : Vb;
-                wc.pdelta = Vd - Vo;
-            }
-        }
+        // The chain writes the window's part of the payload; the rest is
+        // copied after it by the whole wave (coop_payload), and the L4
+        // checksum is refolded with that copy's V change below.
+        if (pay) v.lim = s.wlen;
 #endif
         err = run_chain<ZB_M_WIN>(v, (const uint8_t ZB_LDSP*)nullptr, s.shift, og, nops, wc,
                                   data, lane, &hl, &done, &hw);
     }
+#if ZB_LANE_PAY
+    {
+        // A copy that does not fit the frame failed in the chain before any
+        // byte was written (err != 0): nothing to copy then. The headers fit
+        // the window, so the copy starts at the window end (16-B aligned).
+        const bool go = pay && err == 0;
+        const uint32_t pe = pay_at + pay_len;
+        uintptr_t src = 0;
+        uint32_t cB = 0;
+        if (go) {
+            src = (uintptr_t)data + og.get(nops - 1).data_off + (s.wlen - pay_at);
+            uint32_t Vw = 0;
+#pragma unroll
+            for (uint32_t c = 0; c < ZP_WIN_CH; ++c) Vw += wc.vorig[c];
+            const uint32_t he = (len + s.shift) & 15u;
+            cB = Vw + (he ? range_sum(wc.tail, he, 16u) : 0u) - wc.fsum;
+        }
+        const uint32_t delta = coop_payload(go, s.ga + s.wlen, s.ga + pe, s.ga + len, src, cB,
+                                            lane);
+        if (go) {                                      // refold the L4 checksum
+            const uint32_t k4 = og.kind(nops - 1);
+            const uint32_t at = k4 == ZP_B_TCP ? 16u : k4 == ZP_B_UDP ? 6u : 2u;
+            const uint16_t c = fold_v(wc.cs_V + delta, wc.cs_acc, !((s.ga + wc.cs_l4) & 1));
+            region[s.shift + wc.cs_l4 + at] = (uint8_t)(c >> 8);
+            region[s.shift + wc.cs_l4 + at + 1] = (uint8_t)c;
+        }
+    }
+#endif
     // Write-back of frame bytes [0, hw) from the region: whole 16-B chunks as
     // one store, edge chunks byte by byte (never a byte another lane writes).
     // A store that covers part of a 64-B HBM sector costs ~2.4 x a whole one
@@ -1026,13 +1104,6 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
                 *(ZP_GLOBAL uint8_t*)(a0 + b) = region[b];
         }
     }
-#if ZB_LANE_PAY
-    if (pay_go) {                                      // the payload past the window
-        const uint32_t q0 = s.wlen > pay_at ? s.wlen : pay_at;
-        const uintptr_t src = (uintptr_t)data + og.get(nops - 1).data_off + (q0 - pay_at);
-        gcopy(s.ga + q0, src, pay_at + pay_len - q0);
-    }
-#endif
     if (!fast) return;
     zp_build_result r;
     r.header_len = hl;

@@ -49,7 +49,20 @@ struct zp_ctx {
     uint32_t* d_bstart;
     zp_build_result* d_bres;
     uint32_t* h_bstart;
+    // zp_parse_one: one mapped, coherent pinned block (descriptors, record,
+    // ext entries, frame) the kernel reads and writes in place
+    uint8_t* one_h;
+    uint8_t* one_d;
 };
+
+// zp_parse_one's block: the frame at ONE_FRAME, its descriptor in front, the
+// outputs between them. Frames longer than ONE_MAX take the batch path.
+#define ONE_OFFS 0       // uint64_t: ONE_FRAME
+#define ONE_LENS 8       // uint32_t
+#define ONE_REC 16       // zp_record
+#define ONE_EXT 32       // zp_ext_offsets[2]
+#define ONE_FRAME 64
+#define ONE_MAX (64u << 10)
 
 // Grows a device buffer to at least `need` elements (contents not kept).
 template <typename T>
@@ -90,7 +103,7 @@ extern "C" void zp_ctx_destroy(zp_ctx* c) {
         if (c->s[k]) (void)hipStreamDestroy(c->s[k]);
     }
     (void)hipFree(c->d_bops); (void)hipFree(c->d_bdata); (void)hipFree(c->d_bstart);
-    (void)hipFree(c->d_bres); (void)hipHostFree(c->h_bstart);
+    (void)hipFree(c->d_bres); (void)hipHostFree(c->h_bstart); (void)hipHostFree(c->one_h);
     (void)hipSetDevice(prev);
     free(c);
 }
@@ -256,15 +269,60 @@ extern "C" int zp_parse_batch_host(zp_ctx* c, const uint8_t* arena, uint64_t are
     return parse_host(c, arena, arena_bytes, offs, lens, n, recs, ext, ext ? ext + n : NULL);
 }
 
+// One frame, latency first: the frame is copied into the context's mapped
+// pinned block and the kernel reads it and writes the record and chains
+// there over the host link (no separate DMA copies), then the stream is
+// synchronised: a launch and a wait per call. Frames past ONE_MAX take the
+// chunked batch path.
 extern "C" int zp_parse_one(zp_ctx* c, const uint8_t* frame, uint64_t len,
                             zp_record* record, zp_ext_offsets* ext) {
-    uint64_t off = 0;
-    uint32_t l = (uint32_t)len;
-    if (len > 0xFFFFFFFFull) return -1;
-    static const uint8_t empty[16] = {0};
-    if (!frame) frame = empty;
-    int rc = zp_parse_batch_host(c, frame, len, &off, &l, 1, record, ext);
-    if (rc) return rc;
+    if (!c || !record || len > 0xFFFFFFFFull || (!frame && len)) return -1;
+    if (len > ONE_MAX) {
+        uint64_t off = 0;
+        uint32_t l = (uint32_t)len;
+        const int rc = zp_parse_batch_host(c, frame, len, &off, &l, 1, record, ext);
+        return rc ? rc : record->err;
+    }
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    if (hipSetDevice(c->device) != hipSuccess) return -2;
+    hipError_t e = hipSuccess;
+    if (!c->one_h) {
+        e = hipHostMalloc((void**)&c->one_h, ONE_FRAME + ONE_MAX + 64,
+                          hipHostMallocMapped | hipHostMallocCoherent);
+        if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&c->one_d, c->one_h, 0);
+        if (e != hipSuccess) {
+            (void)hipHostFree(c->one_h);
+            c->one_h = c->one_d = NULL;
+        }
+    }
+    if (e == hipSuccess) {
+        uint8_t* h = c->one_h;
+        const uint64_t at = ONE_FRAME;
+        const uint32_t l = (uint32_t)len;
+        memcpy(h + ONE_OFFS, &at, 8);
+        memcpy(h + ONE_LENS, &l, 4);
+        if (len) memcpy(h + ONE_FRAME, frame, len);
+        const int rc = zp_parse_batch_device(c->one_d, (const uint64_t*)(c->one_d + ONE_OFFS),
+                                             (const uint32_t*)(c->one_d + ONE_LENS), 1,
+                                             (zp_record*)(c->one_d + ONE_REC),
+                                             (zp_ext_offsets*)(c->one_d + ONE_EXT), c->s[0]);
+        if (rc) { (void)hipSetDevice(prev); return rc; }
+        e = hipStreamSynchronize(c->s[0]);
+    }
+    (void)hipSetDevice(prev);
+    if (e != hipSuccess) {
+        snprintf(g_ctx_error, ERRBUF_LEN, "zp_parse_one: %s", hipGetErrorString(e));
+        return -2;
+    }
+    memcpy(record, c->one_h + ONE_REC, sizeof(zp_record));
+    if (ext) {
+        // entries are defined only where the record flags them (zero_packet.h)
+        const zp_ext_offsets* x = (const zp_ext_offsets*)(c->one_h + ONE_EXT);
+        memset(ext, 0, 2 * sizeof(zp_ext_offsets));
+        if (record->flags & ZP_F_EXT) ext[0] = x[0];
+        if (record->flags & ZP_F_INNER_EXT) ext[1] = x[1];
+    }
     return record->err;
 }
 
