@@ -212,8 +212,14 @@ int zp_parse_batch_host_multi(zp_ctx* const* ctxs, int nctx, const uint8_t* aren
                               const uint32_t* lens, uint64_t n, zp_record* records,
                               zp_ext_offsets* ext);
 /* One frame through the GPU path (PacketParser::parse equivalent). ext: NULL
- * or 2 entries (outer, ip_in_ip chain). Returns the zp_err code (>= 0) or a
- * negative value on HIP failure. */
+ * or 2 entries (outer, ip_in_ip chain; zeroed where the record flags no
+ * chain). Returns the zp_err code (>= 0) or a negative value on HIP failure.
+ * Latency, not throughput: the frame is copied into ctx's mapped pinned
+ * block, the kernel reads it and writes the record there, and the call
+ * waits (~20 us per call on MI355X; the CPU reference
+ * parses a frame in well under 1 us). Callers with a stream of frames
+ * should batch them: the host ring (zp_ring_*) or zp_parse_batch_host /
+ * zp_parse_batch_device. Frames over 64 KiB take the batch host path. */
 int zp_parse_one(zp_ctx* ctx, const uint8_t* frame, uint64_t len,
                  zp_record* record, zp_ext_offsets ext[2]);
 
