@@ -604,3 +604,59 @@ def test_config2_full_batch_exact(zp):
     assert (want["err"] == 0).all() and (lens.cpu().numpy() == 64).all()
     assert got.tobytes() == want.tobytes()
     assert zp.records.ext_match(gext, wext, want)
+
+
+def _fast_ip_probe(f):
+    """zp_parse.hip fast_ip_probe in Python: the frames a wave may take the
+    mixed-stack straight-line path for (every frame of a wave must pass)."""
+    if len(f) < 64:
+        return False
+    t0 = (f[12] << 8) | f[13]
+    hl = 18 if t0 == 0x8100 else (22 if t0 == 0x88A8 else 14)
+    et = (f[hl - 2] << 8) | f[hl - 1]
+    if et == 0x0800:
+        return f[hl] == 0x45
+    return et == 0x86DD and f[hl + 6] not in (0, 43, 44, 51, 60)
+
+
+def test_mixed_stack_path_mutations(zp):
+    """The straight-line path for mixed stacks (fast_ip: 0/1/2 tags, IPv4
+    without options or IPv6 without extensions, one IP-in-IP level, every L4
+    reader) on c5 frames with header bytes mutated (tags, ethertypes,
+    versions, lengths, protocols at both levels, L4 fields), half of them
+    with their checksums refilled so the checks after the checksums and the
+    accept path see unusual values; only frames that pass the path's wave
+    probe are kept, so whole waves take it. Every record equals the oracle's."""
+    from fuzzfix import repair
+    rng = random.Random(5)
+    a, o, l_ = zp.batch.generate_host("c5", 70000, first=31337)
+    frames = []
+    vals = [0, 1, 4, 6, 17, 41, 43, 44, 51, 58, 59, 60, 0x45, 0x46, 0x40, 0x60, 0x65, 0x81, 0x00,
+            0x86, 0xdd, 0x88, 0xa8, 0x08, 0xff, 5, 8, 128, 135]
+    for x, y in zip(o, l_):
+        f = bytearray(a[int(x):int(x) + int(y)].tobytes())
+        if rng.random() < 0.4:
+            for _ in range(rng.randint(1, 2)):
+                j = rng.randrange(12, min(len(f), 120))
+                f[j] = rng.choice(vals) if rng.random() < 0.6 else rng.randrange(256)
+            if rng.random() < 0.5:
+                f = bytearray(repair(bytes(f)))
+        f = bytes(f)
+        if _fast_ip_probe(f):
+            frames.append(f)
+    arena, offs, lens = pack(frames)
+    want, wext = orc.parse_batch(arena, offs, lens)
+    nerr = int((want["err"] != 0).sum())
+    assert len(frames) > 60000 and nerr > 5000 and len(frames) - nerr > 40000
+    assert len(set(want["err"].tolist())) >= 12
+    # accepted frames of every stack the path takes: tags, both versions,
+    # IP-in-IP of both inner versions, the four L4 readers
+    ok = want[want["err"] == 0]
+    F = zp.records
+    for bit in (F.F_IPV4, F.F_IPV6, F.F_IP_IN_IP, F.F_IP_IN_IP_V6, F.F_TCP, F.F_UDP, F.F_ICMPV4,
+                F.F_ICMPV6):
+        assert ((ok["flags"] & bit) != 0).sum() > 100, bit
+    assert len(set(ok["eth_len"].tolist())) == 3
+    for shift in (0, 5):
+        got, gext = gpu_parse(zp, arena, offs, lens, base_shift=shift)
+        assert_same(got, gext, want, wext)
