@@ -139,6 +139,9 @@ struct FrameView {
     uint32_t len;            // frame length
     uint4 xc;                // past the window: one cached 16-B chunk ...
     uint32_t xi;             // ... and its index from A & ~15 (~0: none)
+#ifdef ZP_FB2
+    uint4 xc2;               // A/B: and the chunk after it
+#endif
 };
 
 __device__ __forceinline__ uint4 win_chunk(const FrameView& f, uint32_t c) {
@@ -162,6 +165,17 @@ extern "C" unsigned long long zp_dbg_fb_count(void) {
 }
 #endif
 __device__ __forceinline__ uint4 fb_chunk(FrameView& f, uint32_t c) {
+#ifdef ZP_FB2
+    // A/B: a miss loads chunks c and c + 1 together (the walk moves forward)
+    if (c != f.xi && c != f.xi + 1) {
+        const uintptr_t b = ((uintptr_t)f.g & ~(uintptr_t)15) + 16u * c;
+        const uint32_t last = (f.len + f.shift - 1) >> 4;    // never past the frame's last chunk
+        f.xc = ldg16(b);
+        f.xc2 = c + 1 <= last ? ldg16(b + 16) : f.xc;
+        f.xi = c;
+    }
+    return c == f.xi ? f.xc : f.xc2;
+#else
     if (c != f.xi) {
 #ifdef ZP_DBG_FBCOUNT
         atomicAdd(&zp_fb_count, 1ull);
@@ -170,6 +184,7 @@ __device__ __forceinline__ uint4 fb_chunk(FrameView& f, uint32_t c) {
         f.xi = c;
     }
     return f.xc;
+#endif
 }
 
 __device__ __forceinline__ uint32_t dw_of(uint4 v, uint32_t d) {
