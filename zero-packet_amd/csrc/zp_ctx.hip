@@ -277,26 +277,30 @@ extern "C" int zp_parse_batch_host(zp_ctx* c, const uint8_t* arena, uint64_t are
 extern "C" int zp_parse_one(zp_ctx* c, const uint8_t* frame, uint64_t len,
                             zp_record* record, zp_ext_offsets* ext) {
     if (!c || !record || len > 0xFFFFFFFFull || (!frame && len)) return -1;
-    if (len > ONE_MAX) {
-        uint64_t off = 0;
-        uint32_t l = (uint32_t)len;
-        const int rc = zp_parse_batch_host(c, frame, len, &off, &l, 1, record, ext);
-        return rc ? rc : record->err;
-    }
     int prev = 0;
     (void)hipGetDevice(&prev);
     if (hipSetDevice(c->device) != hipSuccess) return -2;
-    hipError_t e = hipSuccess;
-    if (!c->one_h) {
-        e = hipHostMalloc((void**)&c->one_h, ONE_FRAME + ONE_MAX + 64,
-                          hipHostMallocMapped | hipHostMallocCoherent);
-        if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&c->one_d, c->one_h, 0);
-        if (e != hipSuccess) {
+    if (!c->one_h && len <= ONE_MAX) {
+        hipError_t a = hipHostMalloc((void**)&c->one_h, ONE_FRAME + ONE_MAX + 64,
+                                     hipHostMallocMapped | hipHostMallocCoherent);
+        if (a == hipSuccess) a = hipHostGetDevicePointer((void**)&c->one_d, c->one_h, 0);
+        if (a != hipSuccess) {                      // no mapped block: the batch path below
+            (void)hipGetLastError();
             (void)hipHostFree(c->one_h);
             c->one_h = c->one_d = NULL;
         }
     }
-    if (e == hipSuccess) {
+    if (len > ONE_MAX || !c->one_h) {
+        (void)hipSetDevice(prev);
+        uint64_t off = 0;
+        uint32_t l = (uint32_t)len;
+        static const uint8_t empty[16] = {0};
+        if (ext) memset(ext, 0, 2 * sizeof(zp_ext_offsets));   // unflagged entries: zero
+        const int rc = zp_parse_batch_host(c, frame ? frame : empty, len, &off, &l, 1, record, ext);
+        return rc ? rc : record->err;
+    }
+    hipError_t e = hipSuccess;
+    {
         uint8_t* h = c->one_h;
         const uint64_t at = ONE_FRAME;
         const uint32_t l = (uint32_t)len;
