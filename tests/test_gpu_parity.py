@@ -660,3 +660,31 @@ def test_mixed_stack_path_mutations(zp):
     for shift in (0, 5):
         got, gext = gpu_parse(zp, arena, offs, lens, base_shift=shift)
         assert_same(got, gext, want, wext)
+
+
+def test_parse_one_sizes(zp):
+    """zp_parse_one on both of its paths: frames up to 64 KiB through the
+    mapped block (the kernel reads the frame and writes the record over the
+    host link), longer ones through the batch host path; records and chains
+    equal the oracle's, unflagged chain entries zero."""
+    import ctypes
+    rng = np.random.default_rng(13)
+    a, o, l_ = zp.batch.generate_host("c4", 40, first=77)
+    frames = [a[int(x):int(x) + int(y)].tobytes() for x, y in zip(o, l_)]
+    frames += [_jumbo_ipv6(L, rng, ok, p) for L in (65535, 65536, 65537, 90000)
+               for ok in (True, False) for p in (17, 58)]
+    frames += [b"", b"\x00" * 63]
+    lib = zp._lib.hip()
+    ctx = lib.zp_ctx_create(0, 0)
+    try:
+        for f in frames:
+            rec = np.zeros(1, zp.records.RECORD_DTYPE)
+            ext = np.full((2, 16), 0xA5, np.uint8)
+            buf = ctypes.create_string_buffer(f, max(len(f), 1))
+            rc = lib.zp_parse_one(ctx, ctypes.addressof(buf), len(f), rec.ctypes.data,
+                                  ext.ctypes.data)
+            err, wrec, wext = orc.parse_one(f)
+            assert rc == err and rec.tobytes() == wrec.tobytes(), (len(f), rc, err)
+            assert ext.tobytes() == wext.view(np.uint8).tobytes(), len(f)
+    finally:
+        lib.zp_ctx_destroy(ctx)
