@@ -109,10 +109,11 @@ def rb(rng, k):
     return [rng.randrange(256) for _ in range(k)]
 
 
-def random_chain(zp, rng, valid=True):
+def random_chain(zp, rng, valid=True, pay_max=120):
     """A chain walking the typestate graph with random arguments, plus the
     same chain on tests/pybuilder.py (valid chains only) and a buffer length
-    large enough for it (valid) or anything (invalid)."""
+    large enough for it (valid) or anything (invalid). Payloads are up to
+    pay_max - 1 bytes (past 128 B the GPU copies them as a wave)."""
     C = zp.builder.Chain()
     P = []                                    # pybuilder calls, replayed later
     need = 0
@@ -193,7 +194,7 @@ def random_chain(zp, rng, valid=True):
     l4 = rng.choice(["tcp", "udp", "icmp"])
     pay = None
     if rng.random() < 0.6:
-        pay = rb(rng, rng.randrange(0, 120))
+        pay = rb(rng, rng.randrange(0, pay_max))
     if l4 == "tcp":
         doff = rng.choice([5, 6, 8]) if valid else rng.choice([5, 15, 0, 2])
         both("tcp", rb(rng, addr), rng.randrange(65536), rb(rng, addr), rng.randrange(65536),
@@ -221,11 +222,12 @@ def replay_pybuilder(P, size, fill):
     return b.build()
 
 
-def test_oracle_builder_vs_pybuilder(zp):
-    rng = random.Random(2024)
+@pytest.mark.parametrize("pay_max", [120, 1500])
+def test_oracle_builder_vs_pybuilder(zp, pay_max):
+    rng = random.Random(2024 + pay_max)
     chains, pys, lens, fills = [], [], [], []
     for _ in range(600):
-        c, p, need = random_chain(zp, rng, valid=True)
+        c, p, need = random_chain(zp, rng, valid=True, pay_max=pay_max)
         size = need + rng.randrange(0, 200)
         chains.append(c); pys.append(p); lens.append(size)
         fills.append(np.array(rb(rng, size), np.uint8))
@@ -319,19 +321,22 @@ def test_oracle_builder_errors(zp):
 # ---- GPU ---------------------------------------------------------------------
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("seed,big,gap", [(1, False, 5), (2, True, 5), (3, False, 0),
-                                          (4, True, 0)])
-def test_gpu_builder_vs_oracle(zp, seed, big, gap):
+@pytest.mark.parametrize("seed,big,gap,pay_max", [(1, False, 5, 120), (2, True, 5, 120),
+                                                  (3, False, 0, 120), (4, True, 0, 120),
+                                                  (5, True, 3, 1500), (6, False, 0, 1500)])
+def test_gpu_builder_vs_oracle(zp, seed, big, gap, pay_max):
     """gap 0 packs the frames back to back: the lane path then also writes the
     previous frame's unchanged tail bytes of each header's first 64-B sector
     (when that frame's lane writes nothing there), next to pending, failing
-    and truncated neighbours."""
+    and truncated neighbours. pay_max 1500 sends payloads past the window
+    through the wave copy behind every chain shape (extension headers,
+    IP-in-IP, invalid chains)."""
     import torch
     rng = random.Random(seed)
     chains, lens, fills = [], [], []
     for k in range(3000):
         valid = rng.random() < 0.6
-        c, _, need = random_chain(zp, rng, valid=valid)
+        c, _, need = random_chain(zp, rng, valid=valid, pay_max=pay_max)
         r = rng.random()
         if r < 0.15:
             size = rng.randrange(0, need + 1)                  # truncated: error paths

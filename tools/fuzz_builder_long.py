@@ -1,6 +1,7 @@
 """Long GPU-vs-oracle builder fuzz (not part of the test suite): the tests'
 random chains (valid and invalid, truncated buffers, random prior contents,
-frames past the LDS staging) over many seeds; every arena byte and result.
+frames past the LDS staging; odd rounds with payloads up to 1.5 KB, copied
+as a wave) over many seeds; every arena byte and result.
 Usage: python tools/fuzz_builder_long.py [rounds] [chains_per_round]"""
 import importlib
 import os
@@ -28,7 +29,8 @@ def main():
         rng = random.Random(5000 + r)
         chains, lens, fills = [], [], []
         for _ in range(count):
-            c, _, need = random_chain(zp, rng, valid=rng.random() < 0.6)
+            c, _, need = random_chain(zp, rng, valid=rng.random() < 0.6,
+                                      pay_max=1500 if r % 2 else 120)
             x = rng.random()
             size = (rng.randrange(0, need + 1) if x < 0.15 else
                     rng.randrange(2000, 9000) if x < 0.2 else need + rng.randrange(0, 300))

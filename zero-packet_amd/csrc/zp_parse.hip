@@ -828,10 +828,16 @@ __device__ __forceinline__ bool tiny_tile(uint64_t tile, uint32_t len, uintptr_t
     return true;
 }
 
-__device__ __forceinline__ void store_ext(zp_ext_offsets* dst, const zp_ext_offsets& e) {
+__device__ __forceinline__ void store_ext(zp_ext_offsets* base, uint64_t i, const zp_ext_offsets& e) {
     uint4 q;
     memcpy(&q, &e, sizeof e);
-    __builtin_nontemporal_store(zp_u32x4{q.x, q.y, q.z, q.w}, (zp_u32x4*)dst);
+#ifdef ZP_ABL_EXT8
+    // Timing probe only (wrong contents): the store pattern of an 8-B entry
+    // array, entry i at byte 8 * i of the same buffer.
+    __builtin_nontemporal_store(zp_u32x2{q.x ^ q.z, q.y ^ q.w}, (zp_u32x2*)base + i);
+#else
+    __builtin_nontemporal_store(zp_u32x4{q.x, q.y, q.z, q.w}, (zp_u32x4*)(base + i));
+#endif
 }
 
 // Header walk + checksum verdict + record store of a streamed tile; with COLS
@@ -939,9 +945,9 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
         const bool ho = rec.flags & ZP_F_EXT, hi = rec.flags & ZP_F_INNER_EXT;
         const uint64_t mo = __ballot(ho), mi = __ballot(hi);
         if (mo && (ho || __builtin_popcountll(mo) >= ZP_EXT_DENSE))
-            store_ext(ext + p, ho ? w.outer : zp_ext_offsets{});
+            store_ext(ext, p, ho ? w.outer : zp_ext_offsets{});
         if (mi && (hi || __builtin_popcountll(mi) >= ZP_EXT_DENSE))
-            store_ext(ext + n + p, hi ? w.inner : zp_ext_offsets{});
+            store_ext(ext, n + p, hi ? w.inner : zp_ext_offsets{});
     }
     if (COLS) {
         ViewReader rdr{fv};

@@ -24,6 +24,7 @@ static_assert(ZP_WIN % 16 == 0 && ZP_WIN <= 256, "ZP_WIN must be a multiple of 1
 // vmcnt and lgkmcnt, so every LDS wait would also drain in-flight HBM loads.
 #define ZP_GLOBAL __attribute__((address_space(1)))
 typedef unsigned zp_u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned zp_u32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ uint4 ldg16(uintptr_t a) {
     zp_u32x4 v = *(const ZP_GLOBAL zp_u32x4*)a;
