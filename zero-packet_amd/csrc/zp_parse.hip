@@ -376,66 +376,63 @@ __device__ __forceinline__ uint32_t wsum4n(const FrameView& f, uint32_t a, uint3
 // --------------------------------------------------------------------------
 struct Walk {
     zp_record rec;
-    zp_ext_offsets outer;    // ipv6 extension chain (valid iff ZP_F_EXT)
-    zp_ext_offsets inner;    // ip_in_ip IPv6 chain (valid iff ZP_F_INNER_EXT)
+    uint4 outer;             // ipv6 extension chain as a zp_ext_offsets (valid iff ZP_F_EXT)
+    uint4 inner;             // ip_in_ip IPv6 chain (valid iff ZP_F_INNER_EXT)
     uint32_t acc;        // exact pseudo-header accumulator of the innermost IP
     uint32_t l4;         // L4 start (frame offset) when a checksum is pending
     uint8_t pending;     // 1 = L4 checksum still to verify
     uint8_t v6;          // innermost IP is IPv6 (selects the error code)
 };
 
+// Slot k's offset into the dwords of a zp_ext_offsets (len in the low half
+// of dword 0, off[k] at half k + 1): the chain stays in 4 registers.
+__device__ __forceinline__ void put_off(uint32_t (&ed)[4], int slot, uint32_t v) {
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+        if (k == slot) {
+            const int d = (k + 1) >> 1;
+            ed[d] = (k & 1) ? (ed[d] & 0xFFFF0000u) | v : (ed[d] & 0xFFFFu) | (v << 16);
+        }
+}
+
 // Extension-header walk (headers.rs:51-213). Returns 0 or a zp_err.
-// pos = IPv6 payload start; outputs slot offsets relative to pos.
+// pos = IPv6 payload start; outputs slot offsets relative to pos (put_off).
 __device__ __forceinline__ int ext_walk(FrameView& f, uint32_t pos, uint32_t nh,
-                        uint32_t* present, uint16_t off[6], uint32_t* total,
+                        uint32_t* present, uint32_t (&ed)[4], uint32_t* total,
                         uint32_t* final_nh) {
     uint32_t pres = 0, tot = 0, fin = 0;
     uint32_t cur = nh, p = pos;
-    for (int it = 0; it < 8; ++it) {
+    // One instruction stream for the five header types (Hop-by-Hop :90-113,
+    // Routing :117-134, Fragment :138-155, Authentication :159-176,
+    // Destination :180-202): a wave whose frames sit on different types runs
+    // one step per header, not every type's branch with its own dependent
+    // byte read; the next-header and length bytes come in one 16-bit read.
+    // Timing-neutral on c3-c6 against per-type branches
+    // (profiles/r03_kbench_ext_flat.log), kept as the shorter code.
+    for (int it = 0; it < 7; ++it) {                      // <= 6 slots, then a stop
+        const bool hbh = cur == 0, rt = cur == 43, fr = cur == 44, ah = cur == 51, ds = cur == 60;
+        const uint32_t bit = hbh ? 1u : rt ? 2u : fr ? 4u : ah ? 8u : ds ? ((pres & 16u) ? 32u : 16u) : 0u;
+        if (bit == 0 || (pres & bit)) break;              // other header / repeat: Ok (:94-202)
         const uint32_t rem = f.len - p;
-        int slot;
-        uint32_t hl;
-        if (cur == 0) {                                   // Hop-by-Hop (:90-113)
-            if (pres & 1) break;
-            if (pres) return ZP_ERR_EXT_HBH_NOT_FIRST;
-            if (rem < 8) return ZP_ERR_EXT_OPTIONS_TOO_SHORT;
-            hl = (rd8(f, p + 1) + 1) * 8;
-            if (hl > rem) return ZP_ERR_EXT_OPTIONS_EXCEEDS;
-            slot = ZP_EXT_HBH;
-        } else if (cur == 43) {                           // Routing (:117-134)
-            if (pres & 2) break;
-            if (rem < 8) return ZP_ERR_EXT_ROUTING_TOO_SHORT;
-            hl = (rd8(f, p + 1) + 1) * 8;
-            if (hl > rem) return ZP_ERR_EXT_ROUTING_EXCEEDS;
-            slot = ZP_EXT_RT;
-        } else if (cur == 44) {                           // Fragment (:138-155)
-            if (pres & 4) break;
-            if (rem < 8) return ZP_ERR_EXT_FRAGMENT_TOO_SHORT;
-            hl = 8;
-            slot = ZP_EXT_FRAG;
-        } else if (cur == 51) {                           // Authentication (:159-176)
-            if (pres & 8) break;
-            if (rem < 12) return ZP_ERR_EXT_AUTH_TOO_SHORT;
-            hl = (rd8(f, p + 1) + 2) * 4;
-            if (hl > rem) return ZP_ERR_EXT_AUTH_EXCEEDS;
-            slot = ZP_EXT_AH;
-        } else if (cur == 60) {                           // Destination (:180-202)
-            if (pres & 32) break;
-            if (rem < 8) return ZP_ERR_EXT_OPTIONS_TOO_SHORT;
-            hl = (rd8(f, p + 1) + 1) * 8;
-            if (hl > rem) return ZP_ERR_EXT_OPTIONS_EXCEEDS;
-            slot = (pres & 16) ? ZP_EXT_DST2 : ZP_EXT_DST1;
-        } else {
-            break;
-        }
-        const uint32_t next = rd8(f, p);
-        pres |= 1u << slot;
-#pragma unroll
-        for (int k = 0; k < 6; ++k)
-            if (k == slot) off[k] = (uint16_t)(p - pos);   // constant index: stays in VGPRs
+        const uint32_t minl = ah ? 12u : 8u;
+        const bool opt = hbh || ds;
+        if (hbh && pres) return ZP_ERR_EXT_HBH_NOT_FIRST;                 // :98-102
+        if (rem < minl)
+            return opt ? ZP_ERR_EXT_OPTIONS_TOO_SHORT : rt ? ZP_ERR_EXT_ROUTING_TOO_SHORT
+                 : fr ? ZP_ERR_EXT_FRAGMENT_TOO_SHORT : ZP_ERR_EXT_AUTH_TOO_SHORT;
+        const uint32_t t = rd16(f, p);                    // next header, header length field
+        const uint32_t b1 = t & 0xFFu;
+        const uint32_t hl = fr ? 8u : ah ? (b1 + 2) * 4 : (b1 + 1) * 8;
+        if (hl > rem)
+            return opt ? ZP_ERR_EXT_OPTIONS_EXCEEDS : rt ? ZP_ERR_EXT_ROUTING_EXCEEDS
+                       : ZP_ERR_EXT_AUTH_EXCEEDS;
+        const int slot = hbh ? ZP_EXT_HBH : rt ? ZP_EXT_RT : fr ? ZP_EXT_FRAG : ah ? ZP_EXT_AH
+                       : (bit == 32u ? ZP_EXT_DST2 : ZP_EXT_DST1);
+        pres |= bit;
+        put_off(ed, slot, p - pos);
         tot += hl;
-        fin = next;
-        cur = next;
+        fin = t >> 8;
+        cur = fin;
         p += hl;
     }
     *present = pres;
@@ -499,7 +496,7 @@ __device__ __forceinline__ void walk_frame(FrameView& f, Walk& w) {
                 } else {                                              // parser.rs:222-230
                     if (sl < 40) { err = ZP_ERR_IPV6_TOO_SHORT; goto done; }
                     uint32_t pres = 0, tot = 0, fin = 0;
-                    uint16_t eo[6] = {0, 0, 0, 0, 0, 0};
+                    uint32_t eo[4] = {0, 0, 0, 0};
                     const uint32_t nh = rd8(f, pos + 6);
                     const int e = ext_walk(f, pos + 40, nh, &pres, eo, &tot, &fin);  // ipv6.rs:159
                     if (e) { err = e; goto done; }
@@ -511,8 +508,7 @@ __device__ __forceinline__ void walk_frame(FrameView& f, Walk& w) {
                         r.final_nh = (uint8_t)proto;
                         if (pres) {
                             r.flags |= ZP_F_EXT | (pres << 12);
-                            w.outer.len = (uint16_t)tot;
-                            for (int k = 0; k < 6; ++k) w.outer.off[k] = eo[k];
+                            w.outer = make_uint4(eo[0] | tot, eo[1], eo[2], eo[3]);
                         }
                     } else if (level == 1) {
                         r.flags |= ZP_F_IP_IN_IP | ZP_F_IP_IN_IP_V6;
@@ -520,8 +516,7 @@ __device__ __forceinline__ void walk_frame(FrameView& f, Walk& w) {
                         r.inner_final_nh = (uint8_t)proto;
                         if (pres) {
                             r.flags |= ZP_F_INNER_EXT | (pres << 18);
-                            w.inner.len = (uint16_t)tot;
-                            for (int k = 0; k < 6; ++k) w.inner.off[k] = eo[k];
+                            w.inner = make_uint4(eo[0] | tot, eo[1], eo[2], eo[3]);
                         }
                     }
                 }
@@ -828,9 +823,7 @@ __device__ __forceinline__ bool tiny_tile(uint64_t tile, uint32_t len, uintptr_t
     return true;
 }
 
-__device__ __forceinline__ void store_ext(zp_ext_offsets* base, uint64_t i, const zp_ext_offsets& e) {
-    uint4 q;
-    memcpy(&q, &e, sizeof e);
+__device__ __forceinline__ void store_ext(zp_ext_offsets* base, uint64_t i, uint4 q) {
 #ifdef ZP_ABL_EXT8
     // Timing probe only (wrong contents): the store pattern of an 8-B entry
     // array, entry i at byte 8 * i of the same buffer.
@@ -847,7 +840,6 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
                                             zp_record* __restrict__ records,
                                             zp_ext_offsets* __restrict__ ext,
                                             const ColPtrs& cols) {
-    uint4* tail = &lds.win[ZP_WIN_CH * 64];
     const uint8_t* g = (const uint8_t*)s.ga;
     FrameView fv;
     fv.win = &lds.win[0];
@@ -860,8 +852,8 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
     fv.xi = ~0u;
     Walk w;
     w.rec = zp_record{};
-    w.outer = zp_ext_offsets{};
-    w.inner = zp_ext_offsets{};
+    w.outer = make_uint4(0, 0, 0, 0);
+    w.inner = make_uint4(0, 0, 0, 0);
 #ifdef ZP_ABL_FAKE_WALK
     w.pending = s.live && s.len >= 64;
     w.l4 = 42; w.acc = 0; w.v6 = 0;
@@ -905,8 +897,7 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
             const bool odd = (s.ga + w.l4) & 1;
             const uint32_t r = s.rank;
             const uint32_t fsum = lds.cend[r] - (r ? lds.cend[r - 1] : 0u);
-            const uint32_t he = (s.len + s.shift) & 15u;    // bytes of the last chunk in use
-            const uint32_t ex = he ? range_sum(tail[r], he, 16u) : 0u;
+            const uint32_t ex = lds.cex[r];          // V[E, E16), from the stream
 #ifdef ZP_ABL_NO_L4HDR
             ok = csum_ok(w.acc, fsum - ex, odd);                  // timing ablation only
 #else
@@ -945,9 +936,9 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
         const bool ho = rec.flags & ZP_F_EXT, hi = rec.flags & ZP_F_INNER_EXT;
         const uint64_t mo = __ballot(ho), mi = __ballot(hi);
         if (mo && (ho || __builtin_popcountll(mo) >= ZP_EXT_DENSE))
-            store_ext(ext, p, ho ? w.outer : zp_ext_offsets{});
+            store_ext(ext, p, ho ? w.outer : make_uint4(0, 0, 0, 0));
         if (mi && (hi || __builtin_popcountll(mi) >= ZP_EXT_DENSE))
-            store_ext(ext, n + p, hi ? w.inner : zp_ext_offsets{});
+            store_ext(ext, n + p, hi ? w.inner : make_uint4(0, 0, 0, 0));
     }
     if (COLS) {
         ViewReader rdr{fv};
@@ -981,7 +972,6 @@ __device__ __forceinline__ void parse_tiles(const uint8_t* __restrict__ arena,
     WaveLds& lds = lds_all[wid];
     const uintptr_t fallback = (uintptr_t)&zp_safe_chunk;   // dummy loads when T == 0
     uint4* win = &lds.win[0];
-    uint4* tail = &lds.win[ZP_WIN_CH * 64];
     // ZP_K consecutive tiles per wave (one contiguous band of the arena)
 #ifdef ZP_SEG
     // A/B: the grid's blocks interleaved over ZP_SEG contiguous segments of the
@@ -1031,7 +1021,7 @@ __device__ __forceinline__ void parse_tiles(const uint8_t* __restrict__ arena,
             uint32_t ks[ZP_SMALL_G];
             issue_group<ZP_SMALL_G>(0, s.nitems, s.cur, s.R, lane, fallback, vs, ks);
             STAMP(2);
-            consume_group<ZP_SMALL_G>(0, s.nitems, lane, vs, ks, win, tail, lds.cend, s.run);
+            consume_group<ZP_SMALL_G, false, true>(0, s.nitems, lane, vs, ks, win, nullptr, lds.cend, s.run, nullptr, lds.cex);
         } else
 #endif
         {
@@ -1039,10 +1029,10 @@ __device__ __forceinline__ void parse_tiles(const uint8_t* __restrict__ arena,
         uint32_t ka[ZP_G];
         issue_group<ZP_G>(0, s.nitems, s.cur, s.R, lane, fallback, va, ka);
         STAMP(2);
-        consume_group<ZP_G>(0, s.nitems, lane, va, ka, win, tail, lds.cend, s.run);
+        consume_group<ZP_G, false, true>(0, s.nitems, lane, va, ka, win, nullptr, lds.cend, s.run, nullptr, lds.cex);
         for (uint32_t i0 = ZP_G; i0 < s.nitems; i0 += ZP_G) {
             issue_group<ZP_G>(i0, s.nitems, s.cur, s.R, lane, fallback, va, ka);
-            consume_group<ZP_G>(i0, s.nitems, lane, va, ka, win, tail, lds.cend, s.run);
+            consume_group<ZP_G, false, true>(i0, s.nitems, lane, va, ka, win, nullptr, lds.cend, s.run, nullptr, lds.cex);
         }
         }
         wave_lds_fence();                          // LDS written by other lanes
@@ -1052,7 +1042,7 @@ __device__ __forceinline__ void parse_tiles(const uint8_t* __restrict__ arena,
         // (>= 64 B) ever use it.
         {
             const uint32_t r = s.rank & 63u;
-            const uintptr_t org = ((uintptr_t)bperm(s.R.org_hi, r) << 32) | bperm(s.R.org_lo, r);
+            const uintptr_t org = ((uintptr_t)bperm(s.R.org_hi, r) << 32) | (bperm(s.R.org_lo, r) & ~15u);
             s.ga = org + 16ull * bperm(s.R.pfx, r) + s.shift;
         }
 #ifndef ZP_NO_PRIO
