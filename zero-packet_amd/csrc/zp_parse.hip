@@ -840,6 +840,7 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
                                             zp_record* __restrict__ records,
                                             zp_ext_offsets* __restrict__ ext,
                                             const ColPtrs& cols) {
+    uint4* tail = &lds.win[ZP_WIN_CH * 64];
     const uint8_t* g = (const uint8_t*)s.ga;
     FrameView fv;
     fv.win = &lds.win[0];
@@ -897,7 +898,8 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
             const bool odd = (s.ga + w.l4) & 1;
             const uint32_t r = s.rank;
             const uint32_t fsum = lds.cend[r] - (r ? lds.cend[r - 1] : 0u);
-            const uint32_t ex = lds.cex[r];          // V[E, E16), from the stream
+            const uint32_t he = (s.len + s.shift) & 15u;    // bytes of the last chunk in use
+            const uint32_t ex = he ? range_sum(tail[r], he, 16u) : 0u;
 #ifdef ZP_ABL_NO_L4HDR
             ok = csum_ok(w.acc, fsum - ex, odd);                  // timing ablation only
 #else
@@ -972,6 +974,7 @@ __device__ __forceinline__ void parse_tiles(const uint8_t* __restrict__ arena,
     WaveLds& lds = lds_all[wid];
     const uintptr_t fallback = (uintptr_t)&zp_safe_chunk;   // dummy loads when T == 0
     uint4* win = &lds.win[0];
+    uint4* tail = &lds.win[ZP_WIN_CH * 64];
     // ZP_K consecutive tiles per wave (one contiguous band of the arena)
 #ifdef ZP_SEG
     // A/B: the grid's blocks interleaved over ZP_SEG contiguous segments of the
@@ -1021,7 +1024,7 @@ __device__ __forceinline__ void parse_tiles(const uint8_t* __restrict__ arena,
             uint32_t ks[ZP_SMALL_G];
             issue_group<ZP_SMALL_G>(0, s.nitems, s.cur, s.R, lane, fallback, vs, ks);
             STAMP(2);
-            consume_group<ZP_SMALL_G, false, true>(0, s.nitems, lane, vs, ks, win, nullptr, lds.cend, s.run, nullptr, lds.cex);
+            consume_group<ZP_SMALL_G>(0, s.nitems, lane, vs, ks, win, tail, lds.cend, s.run);
         } else
 #endif
         {
@@ -1029,10 +1032,10 @@ __device__ __forceinline__ void parse_tiles(const uint8_t* __restrict__ arena,
         uint32_t ka[ZP_G];
         issue_group<ZP_G>(0, s.nitems, s.cur, s.R, lane, fallback, va, ka);
         STAMP(2);
-        consume_group<ZP_G, false, true>(0, s.nitems, lane, va, ka, win, nullptr, lds.cend, s.run, nullptr, lds.cex);
+        consume_group<ZP_G>(0, s.nitems, lane, va, ka, win, tail, lds.cend, s.run);
         for (uint32_t i0 = ZP_G; i0 < s.nitems; i0 += ZP_G) {
             issue_group<ZP_G>(i0, s.nitems, s.cur, s.R, lane, fallback, va, ka);
-            consume_group<ZP_G, false, true>(i0, s.nitems, lane, va, ka, win, nullptr, lds.cend, s.run, nullptr, lds.cex);
+            consume_group<ZP_G>(i0, s.nitems, lane, va, ka, win, tail, lds.cend, s.run);
         }
         }
         wave_lds_fence();                          // LDS written by other lanes
@@ -1042,7 +1045,7 @@ __device__ __forceinline__ void parse_tiles(const uint8_t* __restrict__ arena,
         // (>= 64 B) ever use it.
         {
             const uint32_t r = s.rank & 63u;
-            const uintptr_t org = ((uintptr_t)bperm(s.R.org_hi, r) << 32) | (bperm(s.R.org_lo, r) & ~15u);
+            const uintptr_t org = ((uintptr_t)bperm(s.R.org_hi, r) << 32) | bperm(s.R.org_lo, r);
             s.ga = org + 16ull * bperm(s.R.pfx, r) + s.shift;
         }
 #ifndef ZP_NO_PRIO
