@@ -22,6 +22,13 @@ Also the checksum.rs:75-133 known-answer tests, and the twelve per-reader
 `reader_getters`: the test buffer's length, every `writer.set_*` call with
 its value, and every `assert_eq!(reader.getter(), value)` with the expected
 value, the `let` bindings and length constants of the test resolved.
+And `debug_impls`: the shape of every Debug output as
+the reference's source writes it: each `impl fmt::Debug` (its debug_struct
+name, field names in order, and what each field formats: a getter, a member,
+a MAC / IPv6 string from bytes_to_mac / bytes_to_ipv6, or IpFormatter), the
+derived Debug structs and enum (PacketParser, ExtensionHeaders, IpInIp) with
+their fields / variants in order, and the helpers' hex alphabet and
+separators (misc.rs:243-290).
 """
 import json
 import os
@@ -131,6 +138,82 @@ def getter_tests(ref):
         out.append({"reader": reader, "source": f"{rel}:{start}-{end + 1}",
                     "buffer_len": buf, "sets": sets, "asserts": asserts})
     return out
+
+
+def _block(text, start):
+    """Text of the brace block opening at or after `start`."""
+    i = text.index("{", start)
+    depth = 0
+    for j in range(i, len(text)):
+        depth += (text[j] == "{") - (text[j] == "}")
+        if depth == 0:
+            return text[i + 1:j]
+    raise ValueError("unbalanced braces")
+
+
+def debug_impls(ref):
+    """The reference's Debug impls and derived Debug types, as data."""
+    files = ["src/datalink/ethernet.rs", "src/datalink/arp.rs", "src/network/ipv4.rs",
+             "src/network/ipv6.rs", "src/network/extensions/options.rs",
+             "src/network/extensions/routing.rs", "src/network/extensions/fragment.rs",
+             "src/network/extensions/authentication.rs", "src/transport/tcp.rs",
+             "src/transport/udp.rs", "src/network/icmpv4.rs", "src/network/icmpv6.rs"]
+    impls = {}
+    for rel in files:
+        text = open(os.path.join(ref, rel)).read()
+        m = re.search(r"impl fmt::Debug for (\w+)<'_> \{", text)
+        line = text[:m.start()].count("\n") + 1
+        body = re.sub(r"//.*", "", _block(text, m.start()))
+        lets = dict(re.findall(r"let (?:mut )?(\w+) = (.+?);", body))
+        name = re.search(r'debug_struct\("(\w+)"\)', body).group(1)
+        fields = []
+        for key, expr in re.findall(r'\.field\("(\w+)",\s*&([^)]*\)?)\)', body):
+            expr = expr.strip()
+            g = re.fullmatch(r"self\.(\w+)\(\)", expr)
+            if g:
+                # with the getter's return type (u8 .. u32, bool, &[u8], Result<..>)
+                ret = re.search(r"pub fn " + g.group(1) + r"\(&self\) -> ([^{]+?)\s*\{", text)
+                fields.append([key, "getter", g.group(1), ret.group(1)])
+                continue
+            g = re.fullmatch(r"self\.(\w+)", expr)
+            if g:
+                fields.append([key, "member", g.group(1)])
+                continue
+            g = re.fullmatch(r"IpFormatter\((\w+)\)", expr)
+            if g:
+                src = re.fullmatch(r"self\.(\w+)\(\)", lets[g.group(1)]).group(1)
+                fields.append([key, "ipv4", src])
+                continue
+            # &s_hex: from_utf8(&s_buf[..s_len]), s_len = bytes_to_X(self.getter(), ..)
+            buf_len = re.search(r"\[\.\.(\w+)\]", lets[expr]).group(1)
+            g = re.fullmatch(r"bytes_to_(mac|ipv6)\(self\.(\w+)\(\), .*", lets[buf_len])
+            fields.append([key, g.group(1), g.group(2)])
+        impls[m.group(1)] = {"struct": name, "fields": fields, "source": f"{rel}:{line}"}
+
+    def derived(rel, kind, name):
+        text = open(os.path.join(ref, rel)).read()
+        m = re.search(r"#\[derive\(Debug\)\]\s*pub " + kind + r" " + name + r"<'a> \{", text)
+        body = re.sub(r"//.*", "", _block(text, m.start()))
+        line = text[:m.start()].count("\n") + 1
+        if kind == "struct":
+            items = re.findall(r"pub (\w+):", body)
+        else:
+            items = re.findall(r"(\w+)\(\w+<'a>\)", body)
+        return {"items": items, "source": f"{rel}:{line}"}
+
+    misc = open(os.path.join(ref, "src/misc.rs")).read()
+    fmt_ip = re.search(r'impl fmt::Debug for IpFormatter<\'_> \{', misc)
+    helpers = {
+        "hex_chars": re.findall(r'HEX_CHARS: &\[u8; 16\] = b"([0-9a-f]+)"', misc),
+        "mac_separator_every": 1 if "if i != 0" in _block(misc, misc.index("fn bytes_to_mac")) else None,
+        "ipv6_separator_every": 2 if "i % 2 == 0 && i != 0" in _block(misc, misc.index("fn bytes_to_ipv6")) else None,
+        "ipv4_format": re.search(r'write!\(f, "([^"]+)"', _block(misc, fmt_ip.start())).group(1),
+    }
+    return {"impls": impls,
+            "PacketParser": derived("src/packet/parser.rs", "struct", "PacketParser"),
+            "ExtensionHeaders": derived("src/network/extensions/headers.rs", "struct", "ExtensionHeaders"),
+            "IpInIp": derived("src/misc.rs", "enum", "IpInIp"),
+            "helpers": helpers}
 
 
 def main(ref):
@@ -310,7 +393,7 @@ def main(ref):
            "reference": "J-Schoepplenberg/zero-packet 0.1.0",
            "fixtures": fixtures, "builder_vectors": builder_vectors,
            "checksum_kats": kats, "pseudo_header_kat": pseudo,
-           "reader_getters": getter_tests(ref)}
+           "reader_getters": getter_tests(ref), "debug_impls": debug_impls(ref)}
     with open(os.path.join(HERE, "parse_golden.json"), "w") as fh:
         json.dump(out, fh, indent=1)
     print(f"wrote {len(fixtures)} fixtures, {len(builder_vectors)} builder vectors, "
