@@ -11,6 +11,9 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 NAMES = ["desc+setup", "issue0", "stream", "walk+verdict"]
+# builds with the tile_finish stamps (5: walk done, 6: verdict done)
+NAMES_FINE = ["desc+setup", "issue0", "stream", "walk", "verdict", "stores"]
+ORDER_FINE = [0, 1, 2, 3, 5, 6, 4]
 
 
 def main():
@@ -37,7 +40,10 @@ def main():
             run()
             torch.cuda.synchronize()
             lib.zp_stamps_set(None)
-            t = buf.view(nw, 8).cpu().numpy().astype(np.int64)[:, :len(NAMES) + 1] * 10  # ns
+            t = buf.view(nw, 8).cpu().numpy().astype(np.int64) * 10  # ns
+            fine = bool((t[:, 5] > 0).all() and (t[:, 6] > 0).all())
+            names = NAMES_FINE if fine else NAMES
+            t = t[:, ORDER_FINE] if fine else t[:, :len(NAMES) + 1]
             d = np.diff(t, axis=1)
             life = t[:, -1] - t[:, 0]
             kern = t[:, -1].max() - t[:, 0].min()
@@ -47,7 +53,7 @@ def main():
                   f"{np.percentile(life, 99)/1e3:.1f}), mean resident waves "
                   f"{life.sum()/kern:.0f}", flush=True)
             print("   " + "  ".join(f"{nm} {d[:, i].mean()/1e3:.2f}us ({100*d[:, i].mean()/life.mean():.0f}%)"
-                                     for i, nm in enumerate(NAMES)), flush=True)
+                                     for i, nm in enumerate(names)), flush=True)
             del arena, offs, lens, rec, ext, buf
             torch.cuda.empty_cache()
 

@@ -842,6 +842,9 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
                                             const ColPtrs& cols) {
     uint4* tail = &lds.win[ZP_WIN_CH * 64];
     const uint8_t* g = (const uint8_t*)s.ga;
+#ifdef ZP_STAMPS
+    const uint64_t wave_id = s.tile;
+#endif
     FrameView fv;
     fv.win = &lds.win[0];
     fv.g = g;
@@ -886,6 +889,7 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
         }
     }
 #endif
+    STAMP(5);
     if (!s.live) return;
     // The frame's stream sum covers the whole chunks [A & ~15, E16):
     // L4 sum = that - V[A & ~15, A + l4) - V[E, E16).
@@ -911,6 +915,7 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
             rec.err = (uint8_t)(w.v6 ? ZP_ERR_IPV6_L4_CHECKSUM : ZP_ERR_IPV4_L4_CHECKSUM);
         }
     }
+    STAMP(6);
     static_assert(sizeof(zp_record) == 16 && sizeof(zp_ext_offsets) == 16, "16-B records");
     const uint64_t p = s.tile * 64 + lane;
 #ifdef ZP_ABL_NOREC
