@@ -34,7 +34,11 @@ def main():
                     help="every frame copies from blob offset 0 (L2-resident source; round 2)")
     ap.add_argument("--oracle-sample", type=int, default=2000,
                     help="frames compared byte for byte with the oracle builder")
+    ap.add_argument("--stamps", action="store_true",
+                    help="phase shares from tools/variants/libzb_stamps.so (ZB_STAMPS build)")
     args = ap.parse_args()
+    if args.stamps and "stamps" not in args.variants.split(","):
+        args.variants = ",".join([v for v in args.variants.split(",") if v] + ["stamps"])
     zp = importlib.import_module("zero-packet_amd")
     B = zp.builder
     d = torch.device("cuda:0")
@@ -104,7 +108,50 @@ def main():
         l_.zp_build_batch_device.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_uint64] + \
             [ctypes.c_void_p] * 5
         libs.append((v, l_))
+    # The write floor at HBM granularity: every frame's written range
+    # [A, A + headers + payload) rounded out to whole 64-B sectors (the
+    # granularity of WRITE_SIZE / TCC_EA0_WRREQ), sectors shared by
+    # neighbouring frames counted once.
+    hlen = 14 + 20 + np.where(tcp, 20, 8)
+    a0 = offs.cpu().numpy().astype(np.int64) + int(arena.data_ptr() % 64)
+    s0, s1 = a0 // 64, (a0 + hlen + pay - 1) // 64
+    order = np.argsort(s0)
+    s0, s1 = s0[order], s1[order]
+    prev_end = np.concatenate([[-1], np.maximum.accumulate(s1)[:-1]])
+    sector_bytes = int(np.maximum(s1 - np.maximum(s0, prev_end + 1) + 1, 0).sum()) * 64
+    exact_write = int(hlen.sum() + pay.sum())
+    print(f"write floor: {exact_write / 1e9:.3f} GB of header/payload bytes, "
+          f"{sector_bytes / 1e9:.3f} GB in whole 64-B sectors "
+          f"({sector_bytes / exact_write:.2f} x)", flush=True)
     s = torch.cuda.current_stream(d)
+    if args.stamps:
+        # phase shares of the lane kernel from the ZB_STAMPS build
+        # (tools/build_variants.sh "b-stamps:-DZB_STAMPS")
+        l_ = dict(libs)["stamps"]
+        l_.zb_stamps_set.argtypes = [ctypes.c_void_p]
+        nw = (n + 63) // 64
+        sb = torch.zeros(nw * 8, dtype=torch.int64, device=d)
+        snap = arena.clone()
+        for k in range(3):
+            arena.copy_(snap)
+            l_.zb_stamps_set(ctypes.c_void_p(sb.data_ptr()) if k == 2 else None)
+            l_.zp_build_batch_device(arena.data_ptr(), offs.data_ptr(), lens.data_ptr(), n,
+                                     t_ops.data_ptr(), t_start.data_ptr(), t_data.data_ptr(),
+                                     res.data_ptr(), s.cuda_stream)
+            torch.cuda.synchronize()
+        l_.zb_stamps_set(None)
+        t = sb.view(nw, 8).cpu().numpy()[:, :6].astype(np.int64) * 10       # ns
+        dd = np.diff(t, axis=1)
+        life = t[:, 5] - t[:, 0]
+        span = t[:, 5].max() - t[:, 0].min()
+        names = ["stream", "chain", "copy pass 1", "copy pass 2", "write-back"]
+        print(f"stamps P={args.payload}: span {span / 1e6:.3f} ms, wave life {life.mean() / 1e3:.1f} us, "
+              f"resident {life.sum() / span:.0f}; " +
+              "  ".join(f"{nm} {dd[:, i].mean() / 1e3:.2f}us ({100 * dd[:, i].mean() / life.mean():.0f}%)"
+                        for i, nm in enumerate(names)), flush=True)
+        arena.copy_(snap)
+        del snap, sb
+        libs = [x for x in libs if x[0] != "stamps"]
     snapshot = arena.clone()
     blob_read = int(pay.sum()) if args.payload and not args.shared_blob else 0
     errs = 0
@@ -131,7 +178,7 @@ def main():
         torch.cuda.synchronize()
         ms = float(np.median([a.elapsed_time(b) for a, b in ev]))
         nbytes = int(ln.sum())
-        hdr = n * 54 + int(pay.sum())
+        hdr = exact_write
         opb = int(t_ops.numel() + t_start.numel() * 4)
         alg = nbytes + hdr + blob_read
         blob = " shared-blob" if args.shared_blob else ""

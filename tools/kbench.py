@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--membw", action="store_true")
+    ap.add_argument("--tiles", action="store_true",
+                    help="read ceiling of the parse kernel's tile pattern (tools/membw.hip)")
     ap.add_argument("--no-base", action="store_true", help="time only --variants (PMC runs)")
     ap.add_argument("--columns", action="store_true", help="also time zp_extract_columns_device")
     ap.add_argument("--col-variants", default="",
@@ -100,6 +102,28 @@ def main():
                 print(f"membw region2={region >> 10}KiB {label}: "
                       f"{nbytes / (np.median(ms) * 1e-3) / 1e9:.0f} GB/s", flush=True)
         del buf, rout
+        torch.cuda.empty_cache()
+    if args.tiles:
+        # The parse kernel's access pattern without its work (tools/membw.hip
+        # read_tiles): one wave per tile-sized region, 1 KiB loads in groups
+        # of 8, 8,960 B of LDS per wave, and a 1 KiB record store per wave.
+        mb = ctypes.CDLL(os.path.join(ROOT, "tools", "libmembw.so"))
+        mb.membw_tiles.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                   ctypes.c_uint64, ctypes.c_int, ctypes.c_uint32,
+                                   ctypes.c_void_p]
+        buf = torch.randint(0, 255, (12 << 30,), dtype=torch.uint8, device=dev)
+        out = torch.zeros((12 << 30) // 4096 * 64 * 4 + 64, dtype=torch.int32, device=dev)
+        for label, region in (("c5 tile (64 x 354.3 B)", 22672), ("c4 tile (64 x 797 B)", 51008),
+                              ("c3 tile (64 x 781.6 B)", 50016), ("16 KiB", 16384),
+                              ("c2 tile (64 x 64 B)", 4096)):
+            for rec in (0, 1):
+                ms = time_launches(lambda: mb.membw_tiles(buf.data_ptr(), buf.numel(),
+                                                          out.data_ptr(), region, rec, 8960,
+                                                          None), 10)
+                nbytes = buf.numel() // region * region
+                print(f"tiles {label:24s} records={rec}: {np.median(ms):.3f} ms "
+                      f"{nbytes / (np.median(ms) * 1e-3) / 1e9:.0f} GB/s", flush=True)
+        del buf, out
         torch.cuda.empty_cache()
     if args.c2cold:
         n = 1 << 20

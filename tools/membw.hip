@@ -181,3 +181,53 @@ extern "C" int membw_write(void* p, uint64_t lines, int lg16, int off16, int nt,
                            lg16, off16, 7u);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+
+// The parse kernel's access pattern without its work: one 64-lane workgroup
+// per region (a tile), 1 KiB nontemporal wave loads in groups of 8, the
+// parse kernel's LDS footprint per workgroup (so the same 18 waves fit a CU),
+// and, with REC, one 16-B nontemporal store per lane at the end (the tile's
+// records, 1 KiB per wave). Regions need not be multiples of 1 KiB: the last
+// item re-reads inside the region, like the stream's clamped items.
+template <bool REC>
+__global__ void __launch_bounds__(64) read_tiles(const uint8_t* __restrict__ p, uint64_t region,
+                                                 uint64_t nreg, uint32_t* __restrict__ out,
+                                                 uint32_t lds_bytes) {
+    extern __shared__ uint32_t lds[];
+    const int lane = threadIdx.x;
+    const uint64_t w = blockIdx.x;
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    const uint8_t* base = p + w * region;
+    const uint64_t nch = region / 16, items = (nch + 63) / 64;
+    uint32_t acc = 0;
+    for (uint64_t i = 0; i < items; i += 8) {
+        u32x4 v[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            uint64_t c = (i + q) * 64 + lane;
+            c = c < nch ? c : nch - 1;
+            v[q] = __builtin_nontemporal_load((const __attribute__((address_space(1))) u32x4*)(base + c * 16));
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc += v[q].x ^ v[q].y ^ v[q].z ^ v[q].w;
+    }
+    lds[lane] = acc;                                   // the LDS is really allocated
+    __builtin_amdgcn_wave_barrier();
+    acc += lds[(lane + 1) & 63] + lds_bytes;
+    if (REC) {
+        u32x4 r = {acc, acc, acc, acc};
+        __builtin_nontemporal_store(r, (u32x4*)(out + (w * 64 + lane) * 4));
+    } else if (acc == 0x12345678u) {
+        out[w * 64 + lane] = acc;
+    }
+}
+
+extern "C" int membw_tiles(const void* p, uint64_t bytes, uint32_t* out, uint64_t region,
+                           int rec, uint32_t lds_bytes, void* stream) {
+    const uint64_t nreg = bytes / region;
+    hipStream_t s = (hipStream_t)stream;
+    if (rec) hipLaunchKernelGGL(read_tiles<true>, dim3((unsigned)nreg), dim3(64), lds_bytes, s,
+                                (const uint8_t*)p, region, nreg, out, lds_bytes);
+    else hipLaunchKernelGGL(read_tiles<false>, dim3((unsigned)nreg), dim3(64), lds_bytes, s,
+                            (const uint8_t*)p, region, nreg, out, lds_bytes);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
