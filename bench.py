@@ -165,7 +165,7 @@ def pcie_inclusive(zp, arena, offs, lens, sample_pkts):
     end = int(o[-1] + ln[-1])
     host = torch.empty(end, dtype=torch.uint8).pin_memory()
     host.copy_(arena[:end])
-    recs = torch.empty((m, 16), dtype=torch.uint8).pin_memory()
+    recs = torch.empty((m, zp.records.RECORD_BYTES), dtype=torch.uint8).pin_memory()
     lib = zp._lib.hip()
     ctx = lib.zp_ctx_create(torch.cuda.current_device(), 256 << 20)
     args = (ctx, host.data_ptr(), end, o.ctypes.data, ln.ctypes.data, m, recs.data_ptr(), None)
@@ -236,7 +236,7 @@ def main():
         first, job_frames, scaling = rank * n, n * world, "weak"
     t0 = time.perf_counter()
     arena, offs, lens = zp.batch.generate(args.config, n, first=first, device=dev)
-    records = torch.empty((n, 16), dtype=torch.uint8, device=dev)
+    records = torch.empty((n, zp.records.RECORD_BYTES), dtype=torch.uint8, device=dev)
     ext = torch.empty((2, n, 16), dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
     total_bytes = int(lens.to(torch.int64).sum().item())
@@ -247,7 +247,7 @@ def main():
     # rejected-frame check below reads its records.
     zp.batch.parse_batch(arena, offs, lens, records, ext, check=True)
     torch.cuda.synchronize()
-    errs = int((records[:, 4] != 0).sum().item())
+    errs = int((zp.batch.record_err(records) != 0).sum().item())
     assert errs == 0, f"{errs} frames rejected (generator/kernel mismatch)"
     for _ in range(args.warmup):
         zp.batch.parse_batch(arena, offs, lens, records, ext, check=False)

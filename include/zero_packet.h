@@ -27,10 +27,12 @@
 extern "C" {
 #endif
 
-#define ZP_ABI_VERSION 3   /* 2: 16-B record, extension chains in the ext side array;
+#define ZP_ABI_VERSION 4   /* 2: 16-B record, extension chains in the ext side array;
                               3: reader-accessor error codes 36-37 (ZP_ERR_COUNT 38,
                                  ZP_STATS_COUNT 62), standalone readers and the
-                                 checksum primitives (zp_reader_new, zp_*checksum*) */
+                                 checksum primitives (zp_reader_new, zp_*checksum*);
+                              4: 8-B record (flags word + packed offsets); the IPv6
+                                 final next header of a chain in its ext entry */
 
 /* ------------------------------------------------------------------------- */
 /* Per-packet parse error codes. One code per DISTINCT reference error string */
@@ -112,47 +114,62 @@ typedef enum zp_err {
 #define ZP_F_INNER_EXT_SLOT(k) (1u << (18 + (k)))  /* inner set             */
 
 /*
- * One parse result, 16 bytes (one dwordx4 store per frame: the record writes
- * are the only HBM writes of the parse and the only traffic besides the
- * frames themselves). All offsets are FRAME offsets (bytes from the first
- * byte of the frame). When err != ZP_OK the reference returns Err and no
- * PacketParser exists: the record is then all zero except `err`.
+ * One parse result, 8 bytes (one dwordx2 store per frame). The record writes
+ * are the only HBM writes of the parse, and writes mixed into the read
+ * stream cost several times their bytes: the 8-B record took
+ * 3-7 % off every configuration against the 16-B record of ABI v2/v3.
  *
- *  - ethernet/arp/ipv4/ipv6 start at offsets 0 / eth_len / eth_len / eth_len.
- *  - final_nh = IPv6Reader::final_next_header() (ipv6.rs:219) of the outer
- *    IPv6, inner_final_nh that of an ip_in_ip IPv6.
- *  - inner_off is the ip_in_ip header.
- *  - l4_off is the start of the single tcp/udp/icmpv4/icmpv6 reader.
- *  - The two Option<ExtensionHeaders> (outer ipv6, ip_in_ip IPv6) go to the
- *    zp_ext_offsets side array (below); ZP_F_EXT / ZP_F_INNER_EXT and the
- *    slot bits say which are Some.
+ *   flags  bits  0-23  ZP_F_* presence and extension-slot bits (above)
+ *          bits 24-25  Ethernet header length: 14 + 4 * code (14 / 18 / 22,
+ *                      ethernet.rs:155-179)
+ *          bits 26-31  err (zp_err; ZP_OK = 0)
+ *   offs   bits  0-17  l4_off: start of the single tcp/udp/icmpv4/icmpv6 reader
+ *          bits 18-31  inner_off: start of the ip_in_ip header (always below
+ *                      16,384: Ethernet 22 + IPv6 40 + the longest chain 9,228)
+ *
+ * All offsets are FRAME offsets (bytes from the first byte of the frame).
+ * ethernet/arp/ipv4/ipv6 start at offsets 0 / eth_len / eth_len / eth_len.
+ * An L4 header that starts at byte ZP_L4_FAR (262,143) or later, which only
+ * an IPv6 jumbogram with dozens of nested maximal headers reaches, is
+ * reported as ZP_L4_FAR; the facades refuse such a record.
+ * When err != ZP_OK the reference returns Err and no PacketParser exists:
+ * the record is then zero except the err bits.
+ *
+ * IPv6Reader::final_next_header() (ipv6.rs:219-227) is not in the record:
+ * for an IPv6 header with an extension chain it is the chain's
+ * final_next_header (headers.rs:26), stored in its zp_ext_offsets entry;
+ * without a chain it is the header's next-header byte (frame offset ip + 6).
  */
 typedef struct zp_record {
     uint32_t flags;
-    uint8_t  err;
-    uint8_t  eth_len;        /* 14, 18 or 22 (ethernet.rs:155-179)        */
-    uint8_t  final_nh;       /* outer IPv6 final next header               */
-    uint8_t  inner_final_nh; /* ip_in_ip IPv6 final next header            */
-    uint32_t inner_off;
-    uint32_t l4_off;
+    uint32_t offs;
 } zp_record;
+
+#define ZP_F_MASK   0x00FFFFFFu
+#define ZP_L4_FAR   0x3FFFFu
+static inline uint32_t zp_rec_err(zp_record r)       { return r.flags >> 26; }
+static inline uint32_t zp_rec_eth_len(zp_record r)   { return 14u + 4u * ((r.flags >> 24) & 3u); }
+static inline uint32_t zp_rec_l4_off(zp_record r)    { return r.offs & ZP_L4_FAR; }
+static inline uint32_t zp_rec_inner_off(zp_record r) { return r.offs >> 18; }
 
 /*
  * One IPv6 extension chain (Some(ExtensionHeaders), headers.rs:19-28), 16 B:
  * len = IPv6Reader::extension_headers_len (ipv6.rs:141), off[k] = start of
- * slot k relative to the IPv6 payload (frame offset ip + 40 + off[k]).
+ * slot k relative to the IPv6 payload (frame offset ip + 40 + off[k]),
+ * final_nh = ExtensionHeaders::final_next_header (headers.rs:26).
  *
  * The ext side array of a batch of n frames holds 2n entries:
  *   ext[i]     the outer ipv6 chain of frame i, valid iff flags & ZP_F_EXT;
  *   ext[n + i] the ip_in_ip IPv6 chain,           valid iff flags & ZP_F_INNER_EXT.
  * Entries whose flag is clear are unspecified (the kernel may leave them
  * untouched or zero them). Passing ext = NULL drops the chains (the records
- * still carry their presence bits, ext lengths excepted).
+ * still carry their presence and slot bits).
  */
 typedef struct zp_ext_offsets {
     uint16_t len;
     uint16_t off[ZP_EXT_SLOTS];
-    uint16_t reserved;
+    uint8_t  final_nh;
+    uint8_t  reserved;
 } zp_ext_offsets;
 
 /* ------------------------------------------------------------------------- */

@@ -443,46 +443,51 @@ struct PacketParser {
     static PacketParser from_record(Bytes frame, const zp_record& r,
                                     const zp_ext_offsets* outer = nullptr,
                                     const zp_ext_offsets* inner = nullptr) {
-        if (r.err) detail::fail(r.err);
-        if (((r.flags & ZP_F_EXT) && !outer) || ((r.flags & ZP_F_INNER_EXT) && !inner))
+        if (zp_rec_err(r)) detail::fail((int)zp_rec_err(r));
+        const uint32_t flags = r.flags & ZP_F_MASK;
+        if (((flags & ZP_F_EXT) && !outer) || ((flags & ZP_F_INNER_EXT) && !inner))
             throw std::invalid_argument("from_record: the record flags an extension chain");
         PacketParser p;
-        const size_t hl = r.eth_len;
-        if (r.flags & ZP_F_ETHERNET) p.ethernet.emplace(frame, hl);
-        if (r.flags & ZP_F_ARP) p.arp.emplace(frame.sub(hl));
-        if (r.flags & ZP_F_IPV4) p.ipv4.emplace(frame.sub(hl));
-        if (r.flags & ZP_F_IPV6) {
+        const size_t hl = zp_rec_eth_len(r), io = zp_rec_inner_off(r);
+        if (flags & ZP_F_ETHERNET) p.ethernet.emplace(frame, hl);
+        if (flags & ZP_F_ARP) p.arp.emplace(frame.sub(hl));
+        if (flags & ZP_F_IPV4) p.ipv4.emplace(frame.sub(hl));
+        if (flags & ZP_F_IPV6) {
             IPv6Reader v6(frame.sub(hl));
-            if (r.flags & ZP_F_EXT) {
-                v6.extension_headers = detail::ext_headers(frame, hl + 40, r.flags, 12, outer->off,
-                                                           outer->len, r.final_nh);
+            if (flags & ZP_F_EXT) {
+                v6.extension_headers = detail::ext_headers(frame, hl + 40, flags, 12, outer->off,
+                                                           outer->len, outer->final_nh);
                 v6.extension_headers_len = outer->len;
             }
             p.ipv6 = v6;
         }
-        if (r.flags & ZP_F_IP_IN_IP) {
+        if (flags & ZP_F_IP_IN_IP) {
             IpInIp ii;
-            if (r.flags & ZP_F_IP_IN_IP_V6) {
+            if (flags & ZP_F_IP_IN_IP_V6) {
                 ii.kind = IpInIp::Kind::Ipv6;
-                IPv6Reader v6(frame.sub(r.inner_off));
-                if (r.flags & ZP_F_INNER_EXT) {
-                    v6.extension_headers = detail::ext_headers(frame, r.inner_off + 40, r.flags, 18,
+                IPv6Reader v6(frame.sub(io));
+                if (flags & ZP_F_INNER_EXT) {
+                    v6.extension_headers = detail::ext_headers(frame, io + 40, flags, 18,
                                                                inner->off, inner->len,
-                                                               r.inner_final_nh);
+                                                               inner->final_nh);
                     v6.extension_headers_len = inner->len;
                 }
                 ii.ipv6 = v6;
             } else {
                 ii.kind = IpInIp::Kind::Ipv4;
-                ii.ipv4.emplace(frame.sub(r.inner_off));
+                ii.ipv4.emplace(frame.sub(io));
             }
             p.ip_in_ip = ii;
         }
-        const Bytes l4 = frame.sub(r.l4_off);
-        if (r.flags & ZP_F_TCP) p.tcp.emplace(l4);
-        if (r.flags & ZP_F_UDP) p.udp.emplace(l4);
-        if (r.flags & ZP_F_ICMPV4) p.icmpv4.emplace(l4);
-        if (r.flags & ZP_F_ICMPV6) p.icmpv6.emplace(l4);
+        const uint32_t l4_off = zp_rec_l4_off(r);
+        constexpr uint32_t l4_any = ZP_F_TCP | ZP_F_UDP | ZP_F_ICMPV4 | ZP_F_ICMPV6;
+        if ((flags & l4_any) && l4_off == ZP_L4_FAR)
+            throw std::invalid_argument("from_record: L4 header past ZP_L4_FAR (not in the record)");
+        const Bytes l4 = frame.sub(l4_off);
+        if (flags & ZP_F_TCP) p.tcp.emplace(l4);
+        if (flags & ZP_F_UDP) p.udp.emplace(l4);
+        if (flags & ZP_F_ICMPV4) p.icmpv4.emplace(l4);
+        if (flags & ZP_F_ICMPV6) p.icmpv6.emplace(l4);
         return p;
     }
 

@@ -352,10 +352,38 @@ static int parse(parser_t* ps, slice_t bytes) {
 
 /* ---- record encoding (include/zero_packet.h) ----------------------------- */
 
+/* The oracle's result of one frame, every field unpacked (the layout of the
+ * ABI v2/v3 record). zpo_pack encodes it as the ABI's 8-B zp_record, which
+ * the tests compare with the GPU's byte for byte; the field-level tests read
+ * this form. final_nh / inner_final_nh: IPv6Reader::final_next_header
+ * (ipv6.rs:219-227) of the outer / ip_in_ip IPv6 (in the ABI: the ext entry
+ * of a chain, else the header's next-header byte). */
+typedef struct zpo_record {
+    uint32_t flags;
+    uint8_t  err, eth_len, final_nh, inner_final_nh;
+    uint32_t inner_off, l4_off;
+} zpo_record;
+
+/* zp_record (include/zero_packet.h): flags | Ethernet code << 24 | err << 26,
+ * l4_off (saturated at ZP_L4_FAR) | inner_off << 18. */
+void zpo_pack(const zpo_record* full, uint64_t n, zp_record* out) {
+    for (uint64_t i = 0; i < n; ++i) {
+        const zpo_record* r = &full[i];
+        if (r->err) {
+            out[i].flags = (uint32_t)r->err << 26;
+            out[i].offs = 0;
+            continue;
+        }
+        out[i].flags = r->flags | ((uint32_t)(r->eth_len - 14) / 4u) << 24;
+        out[i].offs = (r->l4_off < ZP_L4_FAR ? r->l4_off : ZP_L4_FAR) | r->inner_off << 18;
+    }
+}
+
 /* One Option<ExtensionHeaders> (headers.rs:19-28) -> slot bits + a
  * zp_ext_offsets entry (len = extension_headers_len, ipv6.rs:141). */
 static void ext_to_record(const ipv6_t* r, uint32_t shift, uint32_t* flags, zp_ext_offsets* x) {
     x->len = (uint16_t)r->extension_headers_len;
+    x->final_nh = ipv6_final_nh(r);                 /* headers.rs:26 */
     for (int k = 0; k < ZP_EXT_SLOTS; ++k) {
         if (r->ext.h[k].present) {
             *flags |= 1u << (shift + k);
@@ -366,7 +394,7 @@ static void ext_to_record(const ipv6_t* r, uint32_t shift, uint32_t* flags, zp_e
 
 /* One frame: the record, and (xo / xi non-NULL) the outer and ip_in_ip
  * extension chains; entries without a chain are zero. */
-int zpo_parse(const uint8_t* frame, size_t len, zp_record* rec, zp_ext_offsets* xo,
+int zpo_parse(const uint8_t* frame, size_t len, zpo_record* rec, zp_ext_offsets* xo,
               zp_ext_offsets* xi) {
     parser_t ps;
     slice_t s = {frame, len};
@@ -471,7 +499,7 @@ typedef struct {
     const uint8_t* arena;
     const uint64_t* offs;
     const uint32_t* lens;
-    zp_record* recs;
+    zpo_record* recs;
     zp_ext_offsets* ext;        /* 2n entries or NULL */
     uint64_t n, lo, hi;
 } job_t;
@@ -488,7 +516,7 @@ static void* worker(void* a) {
  * (nthreads <= 0: all online cores); ext: NULL or 2n entries laid out as
  * zp_parse_batch_device's. Returns the thread count used. */
 int zpo_parse_batch(const uint8_t* arena, const uint64_t* offs, const uint32_t* lens,
-                    uint64_t n, zp_record* recs, zp_ext_offsets* ext, int nthreads) {
+                    uint64_t n, zpo_record* recs, zp_ext_offsets* ext, int nthreads) {
     if (nthreads <= 0) nthreads = (int)sysconf(_SC_NPROCESSORS_ONLN);
     if (nthreads > 256) nthreads = 256;
     if (nthreads < 1) nthreads = 1;
@@ -566,11 +594,11 @@ static void ip_columns(void* const* cols, uint64_t i, slice_t ip, int v6, uint8_
 }
 
 int zpo_columns(const uint8_t* arena, const uint64_t* offs, const uint32_t* lens,
-                const zp_record* recs, uint64_t n, void* const* cols) {
+                const zpo_record* recs, uint64_t n, void* const* cols) {
     for (int c = 0; c < ZP_COL_COUNT; ++c)
         if (cols[c]) memset(cols[c], 0, n * (uint64_t)col_width[c]);
     for (uint64_t i = 0; i < n; ++i) {
-        const zp_record* r = &recs[i];
+        const zpo_record* r = &recs[i];
         if (r->err || !(r->flags & ZP_F_ETHERNET)) continue;
         slice_t fr = {arena + offs[i], lens[i]};
         const uint32_t hl = r->eth_len;

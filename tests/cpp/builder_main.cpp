@@ -184,7 +184,7 @@ int main() {
             --inflight;
             ring.release(*d);
         }
-        for (const auto& r : want) CHECK(r.err == 0 && (r.flags & ZP_F_UDP));
+        for (const auto& r : want) CHECK(zp_rec_err(r) == 0 && (r.flags & ZP_F_UDP));
         std::printf("OK ring\n");
     }
     std::printf("ALL OK\n");

@@ -13,11 +13,15 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "oracle", "libzp_oracle.so")
 _lib = None
 
+# The oracle's per-frame result, every field unpacked (zpo_record); pack()
+# encodes it as the ABI's 8-B zp_record for byte comparisons with the GPU.
 RECORD_DTYPE = np.dtype([
     ("flags", "<u4"), ("err", "u1"), ("eth_len", "u1"), ("final_nh", "u1"),
     ("inner_final_nh", "u1"), ("inner_off", "<u4"), ("l4_off", "<u4"),
 ])
-EXT_DTYPE = np.dtype([("len", "<u2"), ("off", "<u2", (6,)), ("reserved", "<u2")])
+PACKED_DTYPE = np.dtype([("flags", "<u4"), ("offs", "<u4")])
+EXT_DTYPE = np.dtype([("len", "<u2"), ("off", "<u2", (6,)), ("final_nh", "u1"),
+                      ("reserved", "u1")])
 
 
 def lib():
@@ -35,6 +39,8 @@ def lib():
         l.zpo_internet_checksum.argtypes = [vp, sz, ctypes.c_uint32]
         l.zpo_pseudo_header.restype = ctypes.c_uint32
         l.zpo_pseudo_header.argtypes = [vp, vp, sz, ctypes.c_uint8, sz]
+        l.zpo_pack.restype = None
+        l.zpo_pack.argtypes = [vp, u64, vp]
         _lib = l
     return _lib
 
@@ -48,6 +54,22 @@ def parse_one(frame):
     err = lib().zpo_parse(ctypes.addressof(buf), len(frame), rec.ctypes.data, ext[0:].ctypes.data,
                           ext[1:].ctypes.data)
     return err, rec[0], ext
+
+
+def pack(rec):
+    """oracle records (RECORD_DTYPE) -> the ABI's 8-B records (PACKED_DTYPE)."""
+    rec = np.ascontiguousarray(np.atleast_1d(rec), dtype=RECORD_DTYPE)
+    out = np.zeros(len(rec), PACKED_DTYPE)
+    if len(rec):
+        lib().zpo_pack(rec.ctypes.data, len(rec), out.ctypes.data)
+    return out
+
+
+def parse_one_abi(frame):
+    """parse_one with the record packed as the ABI's zp_record (what the GPU
+    path returns and the facades' from_record takes)."""
+    err, rec, ext = parse_one(frame)
+    return err, pack(rec)[0], ext
 
 
 def record_tuple(rec, ext):

@@ -4,6 +4,7 @@ import ctypes
 import os
 import re
 
+import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -12,6 +13,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def declared(header):
     text = open(os.path.join(ROOT, "include", header)).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    text = re.sub(r"static inline[^{]*\{[^}]*\}", "", text)    # header-only accessors
     return sorted(set(re.findall(r"\b(zp_\w+)\s*\(", text)) - {"zp_err", "zp_record"})
 
 
@@ -50,7 +52,7 @@ def test_err_strings(zp):
         35: "IPv6 encapsulated checksum is invalid.",
     }
     lib = zp._lib.hip()
-    assert lib.zp_abi_version() == 3
+    assert lib.zp_abi_version() == 4
     assert lib.zp_err_str(0) == b""
     for code, s in want.items():
         assert lib.zp_err_str(code).decode() == s
@@ -60,13 +62,21 @@ def test_err_strings(zp):
 
 
 def test_record_layout(zp):
-    """zp_record / zp_ext_offsets (ABI v2) as the numpy dtypes see them."""
+    """zp_record / zp_ext_offsets (ABI v4) as the numpy dtypes see them, and
+    unpack() decoding the packed fields."""
     r, e = zp.records.RECORD_DTYPE, zp.records.EXT_DTYPE
-    assert r.itemsize == 16 and e.itemsize == 16
-    assert r.fields["err"][1] == 4 and r.fields["eth_len"][1] == 5
-    assert r.fields["inner_off"][1] == 8
-    assert r.fields["l4_off"][1] == 12
-    assert e.fields["len"][1] == 0 and e.fields["off"][1] == 2
+    assert r.itemsize == 8 and e.itemsize == 16
+    assert r.fields["flags"][1] == 0 and r.fields["offs"][1] == 4
+    assert e.fields["len"][1] == 0 and e.fields["off"][1] == 2 and e.fields["final_nh"][1] == 14
+    rec = np.zeros(3, r)
+    rec[0] = (zp.records.F_ETHERNET | zp.records.F_IPV6 | zp.records.F_TCP | 2 << 24, 170 | 150 << 18)
+    rec[1] = (29 << 26, 0)                                   # Err(UDP_LENGTH)
+    rec[2] = (zp.records.F_ETHERNET | 1 << 24, zp.records.L4_FAR)
+    u = zp.records.unpack(rec)
+    assert list(u["err"]) == [0, 29, 0] and list(u["eth_len"]) == [22, 0, 18]
+    assert list(u["l4_off"]) == [170, 0, zp.records.L4_FAR] and list(u["inner_off"]) == [150, 0, 0]
+    assert u["flags"][0] == zp.records.F_ETHERNET | zp.records.F_IPV6 | zp.records.F_TCP
+    assert list(zp.records.rec_err(rec)) == [0, 29, 0]
 
 
 def test_no_cpu_fallback(zp):

@@ -38,7 +38,7 @@ PRETTY_UDP = """UdpDatagram {
 def parsed(zp, golden, name):
     fx = next(f for f in golden["fixtures"] if f["name"] == name)
     frame = bytes.fromhex(fx["bytes"])
-    err, rec, ext = orc.parse_one(frame)
+    err, rec, ext = orc.parse_one_abi(frame)
     assert err == 0
     return zp.PacketParser.from_record(frame, rec, ext)
 
@@ -64,7 +64,7 @@ def test_debug_pretty_matches_compact(zp, golden):
     n = 0
     for fx in golden["fixtures"]:
         frame = bytes.fromhex(fx["bytes"])
-        err, rec, ext = orc.parse_one(frame)
+        err, rec, ext = orc.parse_one_abi(frame)
         if err:
             continue
         p = zp.PacketParser.from_record(frame, rec, ext)
@@ -173,7 +173,7 @@ def test_debug_follows_the_reference_impls(zp, golden):
     n = 0
     for fx in golden["fixtures"]:
         frame = bytes.fromhex(fx["bytes"])
-        err, rec, ext = orc.parse_one(frame)
+        err, rec, ext = orc.parse_one_abi(frame)
         if err:
             continue
         p = zp.PacketParser.from_record(frame, rec, ext)

@@ -178,7 +178,7 @@ def column_expect(g, at, l4):
 
 def _records(zp, frames):
     """Frames packed + one record per frame pointing at its fixture header."""
-    rec = np.zeros(len(frames), zp.records.RECORD_DTYPE)
+    rec = np.zeros(len(frames), orc.RECORD_DTYPE)       # unpacked; orc.pack for the ABI
     offs, pos = [], 0
     for i, (g, frame, at, flags, l4, fnh) in enumerate(frames):
         offs.append(pos)
@@ -218,7 +218,7 @@ def test_gpu_columns_return_the_reference_values(zp, golden):
     cols = zp.columns.extract(torch.from_numpy(arena).to(d),
                               torch.from_numpy(offs.astype(np.int64)).to(d),
                               torch.from_numpy(lens.astype(np.int32)).to(d),
-                              torch.from_numpy(rec.view(np.uint8).reshape(-1, 16)).to(d))
+                              torch.from_numpy(orc.pack(rec).view(np.uint8).reshape(-1, 8)).to(d))
     cols = {k: v.cpu().numpy() for k, v in cols.items()}
     get = lambda c, i: c[i].tolist() if c.ndim > 1 else int(c[i])
     assert _check_columns(frames, cols, get) == 38

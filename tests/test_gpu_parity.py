@@ -51,8 +51,8 @@ def gpu_parse(zp, arena, offs, lens, base_shift=0):
 def assert_same(got, got_ext, want, want_ext):
     """Records byte-identical; the extension chains the records flag
     identical (records.ext_match; other ext entries are unspecified)."""
-    g = got.view(np.uint8).reshape(-1, 16)
-    w = want.view(np.uint8).reshape(-1, 16)
+    g = got.view(np.uint8).reshape(-1, 8)
+    w = orc.pack(want).view(np.uint8).reshape(-1, 8)     # the oracle's records, packed
     diff = np.nonzero((g != w).any(1))[0]
     assert len(diff) == 0, (f"{len(diff)} records differ; first {diff[:5]}",
                             got[diff[:3]], want[diff[:3]])
@@ -358,7 +358,7 @@ def test_full_size_properties(zp, config, n):
     arena, offs, lens = zp.batch.generate(config, n, device=dev())
     zeros = lambda: torch.zeros((2, n, 16), dtype=torch.uint8, device=arena.device)
     r1, e1 = zp.batch.parse_batch(arena, offs, lens, ext=zeros())
-    assert int((r1[:, 4] != 0).sum()) == 0
+    assert int((zp.batch.record_err(r1) != 0).sum()) == 0
     r2, e2 = zp.batch.parse_batch(arena, offs, lens, ext=zeros())
     assert torch.equal(r1, r2) and torch.equal(e1, e2)
     idx = torch.randint(0, n, (2000,), device=arena.device, generator=torch.Generator(
@@ -369,7 +369,7 @@ def test_full_size_properties(zp, config, n):
     want, wext = orc.parse_batch(sa, sof, sle)
     got, gext = zp.batch.records_to_numpy(r1[idx], e1[:, idx])
     assert_same(got, gext, want, wext)
-    flags = r1[:, 0:4].contiguous().view(torch.int32)[:, 0]
+    flags = zp.batch.record_flags(r1)
     ipip = (flags & rec.F_IP_IN_IP) != 0
     v6 = torch.where(ipip, (flags & rec.F_IP_IN_IP_V6) != 0, (flags & rec.F_IPV6) != 0)
     want_err = torch.where(v6, ERR["IPV6_L4_CHECKSUM"], ERR["IPV4_L4_CHECKSUM"]).to(torch.uint8)
@@ -380,7 +380,7 @@ def test_full_size_properties(zp, config, n):
     arena[last] ^= 1
     r3, _ = zp.batch.parse_batch(arena, offs, lens)
     torch.cuda.synchronize()
-    assert torch.equal(r3[:, 4], want_err)
+    assert torch.equal(zp.batch.record_err(r3), want_err)
     assert torch.equal(r3[arp], r1[arp])
 
 
@@ -398,7 +398,7 @@ def test_max_size_full_imix_one_gpu(zp):
     arena, offs, lens = zp.batch.generate("c5", n, device=dev())
     assert int(offs[-1].item()) > (1 << 36)
     rec, ext = zp.batch.parse_batch(arena, offs, lens)
-    assert int((rec[:, 4] != 0).sum()) == 0
+    assert int((zp.batch.record_err(rec) != 0).sum()) == 0
     g = torch.Generator(device=arena.device).manual_seed(5)
     idx = torch.cat([torch.randint(0, n, (3000,), device=arena.device, generator=g),
                      torch.arange(n - 1000, n, device=arena.device)])
@@ -427,7 +427,7 @@ def test_descriptor_bounds_refused(zp):
     with pytest.raises(ValueError):
         zp.batch.parse_batch(a, torch.tensor([0, -64], dtype=torch.int64, device=d), good)
     with pytest.raises(ValueError):
-        zp.batch.parse_batch(a, o, good, records=torch.empty((2, 8), dtype=torch.uint8, device=d))
+        zp.batch.parse_batch(a, o, good, records=torch.empty((2, 4), dtype=torch.uint8, device=d))
     with pytest.raises(ValueError):
         zp.batch.parse_batch(a, o, good, ext=torch.empty((2, 2, 16), dtype=torch.uint8))
     with pytest.raises(ValueError):
@@ -602,7 +602,7 @@ def test_config2_full_batch_exact(zp):
     got, gext = zp.batch.records_to_numpy(recs, ext)
     want, wext = orc.parse_batch(arena.cpu().numpy(), offs.cpu().numpy(), lens.cpu().numpy())
     assert (want["err"] == 0).all() and (lens.cpu().numpy() == 64).all()
-    assert got.tobytes() == want.tobytes()
+    assert got.tobytes() == orc.pack(want).tobytes()
     assert zp.records.ext_match(gext, wext, want)
 
 
@@ -684,7 +684,7 @@ def test_parse_one_sizes(zp):
             rc = lib.zp_parse_one(ctx, ctypes.addressof(buf), len(f), rec.ctypes.data,
                                   ext.ctypes.data)
             err, wrec, wext = orc.parse_one(f)
-            assert rc == err and rec.tobytes() == wrec.tobytes(), (len(f), rc, err)
+            assert rc == err and rec.tobytes() == orc.pack(wrec).tobytes(), (len(f), rc, err)
             assert ext.tobytes() == wext.view(np.uint8).tobytes(), len(f)
     finally:
         lib.zp_ctx_destroy(ctx)

@@ -29,7 +29,7 @@ def test_ring_parse_matches_oracle(zp, cfg, slots, slot_bytes):
     want, wext = orc.parse_batch(arena, offs, lens)
     with zp.ring.Ring(0, slots, slot_bytes) as ring:
         got, gext = ring.parse(arena, offs, lens)
-    assert got.tobytes() == want.tobytes()
+    assert got.tobytes() == orc.pack(want).tobytes()
     assert zp.records.ext_match(gext, wext, want)
 
 
@@ -75,7 +75,7 @@ def test_ring_producer_consumer_threads(zp, golden):
     assert not tp.is_alive() and not tc.is_alive()
     assert sorted(results) == list(range(len(batches)))
     for seq, b in enumerate(batches):
-        want = np.array([orc.parse_one(f)[1] for f in b], orc.RECORD_DTYPE)
+        want = orc.pack(np.array([orc.parse_one(f)[1] for f in b], orc.RECORD_DTYPE))
         assert results[seq].tobytes() == want.tobytes(), seq
     ring.close()
 
@@ -102,7 +102,7 @@ def test_ring_misuse(zp):
     s.arena[:64] = 0
     ring.submit(s, 1)
     d = ring.wait()
-    want = orc.parse_one(bytes(64))[1]                  # unknown ethertype 0: Ok, ethernet only
+    want = orc.parse_one_abi(bytes(64))[1]              # unknown ethertype 0: Ok, ethernet only
     assert d.n == 1 and d.records.tobytes() == want.tobytes()
     ring.release(d)
     ring.close()

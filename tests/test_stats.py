@@ -62,8 +62,8 @@ def test_stats_match_oracle(zp, golden):
 @pytest.mark.gpu
 def test_stats_byte_counter_flush(zp):
     """48M synthetic records, 90 % of them with all 24 flag bits set: every
-    lane runs past the 63 trips after which zp_stats_kernel flushes its SWAR
-    byte counters (ST_GRID 512 x 256 lanes x ST_U 4 = 0.5M records per trip),
+    lane runs past the 31 trips after which zp_stats_kernel flushes its SWAR
+    byte counters (ST_GRID 512 x 256 lanes x ST_U 8 = 1M records per trip),
     and without that flush the byte counts (> 255 per lane) would carry into
     the next flag's byte. Counts equal numpy counts of the same records."""
     import torch
@@ -75,9 +75,8 @@ def test_stats_byte_counter_flush(zp):
                         torch.randint(0, 1 << 24, (n,), dtype=torch.int64, device=d))
     err = torch.where(torch.rand(n, device=d) < 0.8, torch.zeros(n, dtype=torch.int64, device=d),
                       torch.randint(0, 36, (n,), dtype=torch.int64, device=d))
-    recs = torch.zeros((n, 16), dtype=torch.uint8, device=d)
-    recs.view(torch.int32)[:, 0] = flags.to(torch.int32)
-    recs[:, 4] = err.to(torch.uint8)
+    recs = torch.zeros((n, 8), dtype=torch.uint8, device=d)
+    recs.view(torch.int32)[:, 0] = (flags | (err << 26)).to(torch.int32)   # err in bits 26-31
     got = zp.stats.count(recs).cpu().numpy()
     f = flags.cpu().numpy()
     want = [int(((f >> b) & 1).sum()) for b in range(24)]
@@ -91,7 +90,7 @@ def test_count_refuses_bad_tensors(zp):
     counts (CPU tensors are refused first: no fallback)."""
     import torch
     with pytest.raises(RuntimeError):
-        zp.stats.count(torch.zeros((4, 16), dtype=torch.uint8))
+        zp.stats.count(torch.zeros((4, 8), dtype=torch.uint8))
 
 
 @pytest.mark.gpu
@@ -102,5 +101,5 @@ def test_count_refuses_bad_device_tensors(zp):
         zp.stats.count(torch.zeros((4, 4), dtype=torch.int32, device=d))
     big = torch.zeros((zp.stats.COUNT, 2), dtype=torch.int64, device=d)
     with pytest.raises(ValueError):                      # strided counts view
-        zp.stats.count(torch.zeros((4, 16), dtype=torch.uint8, device=d), counts=big[:, 0])
+        zp.stats.count(torch.zeros((4, 8), dtype=torch.uint8, device=d), counts=big[:, 0])
     assert int(big.sum().item()) == 0

@@ -30,7 +30,7 @@ def timeit(arena, offs, lens, records, inner, steps, base=None):
         zp.batch.parse_batch(arena, offs, lens, records, inner, check=False)
         b.record(s)
     torch.cuda.synchronize()
-    assert int((records[:, 4] != 0).sum().item()) == 0
+    assert int((zp.batch.record_err(records) != 0).sum().item()) == 0
     t = sorted(a.elapsed_time(b) for a, b in ev)
     return {"mean": round(sum(t) / len(t), 4), "min": round(t[0], 4),
             "med": round(t[len(t) // 2], 4)}
@@ -53,7 +53,7 @@ def main():
     dev = torch.device("cuda", 0)
     arena, offs, lens = zp.batch.generate(a.config, a.packets, device=dev)
     n = a.packets
-    records = torch.empty((n, 16), dtype=torch.uint8, device=dev)
+    records = torch.empty((n, 8), dtype=torch.uint8, device=dev)
     inner = torch.empty((2, n, 16), dtype=torch.uint8, device=dev)
     nb = arena.numel()
     mb = ctypes.CDLL(os.path.join(ROOT, "tools", "libmembw.so"))
@@ -112,19 +112,19 @@ def main():
     if a.colocate:
         # arena and records in ONE allocation: records right after the arena
         # (2 MiB aligned, plus a gap), or right before it
-        rb = n * 16
+        rb = n * 8
         al = 2 << 20
         for k in range(a.copies):
             for gap, before in ((0, False), (64 << 10, False), (al, False), (0, True)):
                 body = (nb + al - 1) // al * al
                 blk = torch.empty(body + gap + rb + al, dtype=torch.uint8, device=dev)
                 if before:
-                    rec2 = blk[:rb].view(n, 16)
+                    rec2 = blk[:rb].view(n, 8)
                     a0 = (rb + gap + al - 1) // al * al
                     ar2 = blk[a0:a0 + nb]
                 else:
                     ar2 = blk[:nb]
-                    rec2 = blk[body + gap:body + gap + rb].view(n, 16)
+                    rec2 = blk[body + gap:body + gap + rb].view(n, 8)
                 ar2.copy_(arena)
                 r = timeit(ar2, offs, lens, rec2, inner, a.steps)
                 sep = timeit(ar2, offs, lens, records, inner, a.steps)
@@ -141,7 +141,7 @@ def main():
         hold = []
         for k in range(a.copies):
             hold.append(torch.empty(97 << 20, dtype=torch.uint8, device=dev))   # shift the next block
-            rec2 = torch.empty((n, 16), dtype=torch.uint8, device=dev)
+            rec2 = torch.empty((n, 8), dtype=torch.uint8, device=dev)
             r = timeit(arena, offs, lens, rec2, inner, a.steps)
             r["rec_ptr"] = hex(rec2.data_ptr())
             s = torch.cuda.current_stream()
@@ -186,7 +186,7 @@ def main():
         for _ in range(3):
             launch()
         r = {"parse_med": bw(launch), "ptr": hex(p.value)}
-        assert int((records[:, 4] != 0).sum().item()) == 0
+        assert int((zp.batch.record_err(records) != 0).sum().item()) == 0
         if not a.parse_only:
             r["region48_ms"] = bw(lambda: mb.membw_region2(p, nb // (48 << 10) * (48 << 10),
                                                            rout.data_ptr(), 48 << 10, 0, None))

@@ -213,7 +213,7 @@ def main():
         assert bad == 0
     recs, _ = zp.batch.parse_batch(arena, offs, lens)
     torch.cuda.synchronize()
-    bad = int((recs[:, 4] != 0).sum())
+    bad = int((zp.batch.record_err(recs) != 0).sum())
     print(f"round trip: {n - bad}/{n} rebuilt frames parse Ok", flush=True)
     assert errs == 0 and bad == 0
 

@@ -34,7 +34,7 @@ def main():
     for cfg in a.configs.split(","):
         n = {"c3": 1 << 24, "c4": 1 << 24, "c5": 1 << 25, "c2": 1 << 20}[cfg]
         arena, offs, lens = zp.batch.generate(cfg, n, device=d)
-        rec = torch.empty((n, 16), dtype=torch.uint8, device=d)
+        rec = torch.empty((n, 8), dtype=torch.uint8, device=d)
         ext = torch.empty((2, n, 16), dtype=torch.uint8, device=d)
         cols = [torch.empty(n * zp.columns.width(c), dtype=torch.uint8, device=d)
                 for c in zp.columns.NAMES]

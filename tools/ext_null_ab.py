@@ -5,7 +5,7 @@ d = torch.device("cuda:0")
 n = 1 << 24
 for cfg in ("c4", "c3"):
     arena, offs, lens = zp.batch.generate(cfg, n, device=d)
-    rec = torch.empty((n, 16), dtype=torch.uint8, device=d)
+    rec = torch.empty((n, 8), dtype=torch.uint8, device=d)
     ext = torch.empty((2, n, 16), dtype=torch.uint8, device=d)
     lib = zp._lib.hip()
     s = torch.cuda.current_stream()

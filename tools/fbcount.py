@@ -16,7 +16,7 @@ def main():
     dev = torch.device("cuda:0")
     for cfg, n in (("c3", 1 << 22), ("c4", 1 << 22), ("c5", 1 << 22)):
         arena, offs, lens = zp.batch.generate(cfg, n, device=dev)
-        rec = torch.empty((n, 16), dtype=torch.uint8, device=dev)
+        rec = torch.empty((n, 8), dtype=torch.uint8, device=dev)
         ext = torch.empty((2, n, 16), dtype=torch.uint8, device=dev)
         for v in sys.argv[1].split(","):
             lib = ctypes.CDLL(os.path.join(ROOT, "tools", "variants", f"libzp_{v}.so"))

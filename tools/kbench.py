@@ -116,19 +116,19 @@ def main():
         for label, region in (("c5 tile (64 x 354.3 B)", 22672), ("c4 tile (64 x 797 B)", 51008),
                               ("c3 tile (64 x 781.6 B)", 50016), ("16 KiB", 16384),
                               ("c2 tile (64 x 64 B)", 4096)):
-            for rec in (0, 1):
+            for rec in (0, 1, 2):                 # no records, 16-B, 8-B records
                 ms = time_launches(lambda: mb.membw_tiles(buf.data_ptr(), buf.numel(),
-                                                          out.data_ptr(), region, rec, 8960,
-                                                          None), 10)
+                                                          out.data_ptr(), region, rec > 0,
+                                                          8960 + (rec == 2), None), 10)
                 nbytes = buf.numel() // region * region
-                print(f"tiles {label:24s} records={rec}: {np.median(ms):.3f} ms "
+                print(f"tiles {label:24s} records={(0, 16, 8)[rec]}B: {np.median(ms):.3f} ms "
                       f"{nbytes / (np.median(ms) * 1e-3) / 1e9:.0f} GB/s", flush=True)
         del buf, out
         torch.cuda.empty_cache()
     if args.c2cold:
         n = 1 << 20
         copies = [zp.batch.generate("c2", n, device=dev) for _ in range(8)]
-        rec = torch.empty((n, 16), dtype=torch.uint8, device=dev)
+        rec = torch.empty((n, 8), dtype=torch.uint8, device=dev)
         lib = zp._lib.hip()
         nbytes = int(copies[0][2].to(torch.int64).sum())
         for label, order in (("warm (same copy)", [0] * 8), ("cold (8 rotating copies)",
@@ -155,6 +155,7 @@ def main():
         cfg, _, nn = cfg.partition(":")            # "c3:1048576": another batch size
         n = int(nn) if nn else sizes[cfg]
         arena, offs, lens = zp.batch.generate(cfg, n, device=dev)
+        # 16 B per frame: room for variants built with the ABI v2/v3 record
         rec = torch.empty((n, 16), dtype=torch.uint8, device=dev)
         ext = torch.empty((2, n, 16), dtype=torch.uint8, device=dev)
         nbytes = int(lens.to(torch.int64).sum())
@@ -175,6 +176,7 @@ def main():
             med = float(np.median(ms))
             print(f"{cfg} {name:>12}: {med:8.3f} ms  {nbytes / med / 1e6:7.0f} GB/s  "
                   f"{n / med / 1e3:8.0f} Mpkt/s  (min {min(ms):.3f})", flush=True)
+        rec = rec.view(-1)[:n * zp.records.RECORD_BYTES].view(n, zp.records.RECORD_BYTES)
         if args.columns:
             zp.batch.parse_batch(arena, offs, lens, rec, ext, check=False)
             for label, names in (("all", zp.columns.NAMES),

@@ -213,7 +213,11 @@ __global__ void __launch_bounds__(64) read_tiles(const uint8_t* __restrict__ p, 
     lds[lane] = acc;                                   // the LDS is really allocated
     __builtin_amdgcn_wave_barrier();
     acc += lds[(lane + 1) & 63] + lds_bytes;
-    if (REC) {
+    if (REC && lds_bytes & 1) {                        // 8-B records (lds_bytes odd)
+        typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+        u32x2 r = {acc, acc};
+        __builtin_nontemporal_store(r, (u32x2*)(out + (w * 64 + lane) * 2));
+    } else if (REC) {
         u32x4 r = {acc, acc, acc, acc};
         __builtin_nontemporal_store(r, (u32x4*)(out + (w * 64 + lane) * 4));
     } else if (acc == 0x12345678u) {

@@ -32,7 +32,7 @@ def main():
     n = {"c2": 1 << 20, "c3": 1 << 24, "c4": 1 << 24, "c5": 1 << 25}[cfg]
     d = torch.device("cuda:0")
     arena, offs, lens = zp.batch.generate(cfg, n, device=d)
-    rec = torch.empty((n, 16), dtype=torch.uint8, device=d)
+    rec = torch.empty((n, 8), dtype=torch.uint8, device=d)
     ext = torch.empty((2, n, 16), dtype=torch.uint8, device=d)
     for name in names:
         lib = zp._lib.hip() if name == "base" else ctypes.CDLL(

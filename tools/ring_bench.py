@@ -90,7 +90,7 @@ def main():
     ring.close()
     # synchronous host batch path on pinned memory, same frames
     host = torch.from_numpy(arena).pin_memory()
-    recs = torch.empty((len(offs), 16), dtype=torch.uint8).pin_memory()
+    recs = torch.empty((len(offs), 8), dtype=torch.uint8).pin_memory()
     lib = zp._lib.hip()
     ctx = lib.zp_ctx_create(0, 256 << 20)
     a = (ctx, host.data_ptr(), len(arena), offs.ctypes.data, lens.ctypes.data, len(offs),

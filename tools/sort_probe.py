@@ -58,7 +58,7 @@ def main():
     dev = torch.device("cuda:0")
     n = args.packets
     arena, offs, lens = zp.batch.generate(args.config, n, device=dev)
-    rec = torch.empty((n, 16), dtype=torch.uint8, device=dev)
+    rec = torch.empty((n, 8), dtype=torch.uint8, device=dev)
     ext = torch.empty((2, n, 16), dtype=torch.uint8, device=dev)
     nbytes = int(lens.to(torch.int64).sum())
 

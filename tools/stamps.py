@@ -27,7 +27,7 @@ def main():
         for cfg in sys.argv[2].split(","):
             n = {"c3": 1 << 24, "c4": 1 << 24, "c5": 1 << 25, "c2": 1 << 20}[cfg]
             arena, offs, lens = zp.batch.generate(cfg, n, device=dev)
-            rec = torch.empty((n, 16), dtype=torch.uint8, device=dev)
+            rec = torch.empty((n, 8), dtype=torch.uint8, device=dev)
             ext = torch.empty((2, n, 16), dtype=torch.uint8, device=dev)
             nw = (n + 63) // 64
             buf = torch.zeros(nw * 8, dtype=torch.int64, device=dev)

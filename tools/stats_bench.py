@@ -1,4 +1,4 @@
-"""Timing of zp_stats_device over one c3 batch's records (16M x 16 B)."""
+"""Timing of zp_stats_device over one c3 batch's records (16M x 8 B)."""
 import importlib
 import os
 import sys
@@ -41,7 +41,7 @@ def main():
             torch.cuda.synchronize()
             ms = sorted(a.elapsed_time(b) for a, b in ev)[10]
             print(f"zp_stats_device [{name}], {n} records: {ms * 1e3:.1f} us, "
-                  f"{n * 16 / ms / 1e6:.0f} GB/s of records, {n / ms / 1e6:.1f} Gpkt/s", flush=True)
+                  f"{n * 8 / ms / 1e6:.0f} GB/s of records, {n / ms / 1e6:.1f} Gpkt/s", flush=True)
     print(zp.stats.to_dict(zp.stats.count(r)), flush=True)
 
 

@@ -145,8 +145,19 @@ def generate_host(config, n, seed=SEED, first=0, nthreads=0, pad=64):
     return arena, offs, lens
 
 
+def record_err(records):
+    """err codes of raw records (uint8 [n, 8], torch or numpy): bits 26-31 of
+    the flags word, i.e. byte 3 >> 2 (include/zero_packet.h)."""
+    return records[:, 3] >> 2
+
+
+def record_flags(records):
+    """ZP_F_* bits of raw records (uint8 [n, 8], torch): int32 [n]."""
+    return records[:, 0:4].contiguous().view(torch.int32)[:, 0] & 0x00FFFFFF
+
+
 def records_to_numpy(records, ext=None):
-    """uint8 [n, 16] (device or host) -> structured numpy (RECORD_DTYPE) [n];
+    """uint8 [n, 8] (device or host) -> structured numpy (RECORD_DTYPE) [n];
     with ext (uint8 [2, n, 16]) also the chains as EXT_DTYPE [2, n]."""
     r = records.cpu().numpy() if isinstance(records, torch.Tensor) else records
     rec = np.ascontiguousarray(r).view(RECORD_DTYPE).reshape(-1)

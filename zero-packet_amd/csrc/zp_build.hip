@@ -780,6 +780,22 @@ __device__ __forceinline__ uint32_t chain_extent(const OpGlobal& ops, uint32_t n
 #define ZB_LANE_PAY 1          // payload copies past the window on the lane path
 #endif
 
+// Diagnostic build only (-DZB_STAMPS, tools/build_bench.py --stamps): per-wave
+// s_memrealtime stamps at the phase boundaries of zp_build_fast_kernel.
+#ifdef ZB_STAMPS
+__device__ unsigned long long* zb_stamp_buf;
+#define ZB_STAMP(i)                                                               \
+    do {                                                                          \
+        const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();           \
+        if (zb_stamp_buf && threadIdx.x == 0) zb_stamp_buf[blockIdx.x * 8 + (i)] = t_; \
+    } while (0)
+extern "C" int zb_stamps_set(void* p) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(zb_stamp_buf), &p, sizeof p) == hipSuccess ? 0 : -1;
+}
+#else
+#define ZB_STAMP(i) do {} while (0)
+#endif
+
 // Wave-cooperative segments: lane j owns cnt_j chunks; the wave walks the
 // concatenation of all lanes' chunks in items of 64 (lane l of item i takes
 // virtual chunk 64 i + l, its owner j found by a binary search over the
@@ -873,6 +889,7 @@ __device__ __forceinline__ uint32_t coop_payload(bool go, uintptr_t D0, uintptr_
             const uint32_t v = range_sum(c.q, c.l, c.h);
             return c.neg ? 0u - v : v;
         });
+    ZB_STAMP(3);
     // pass 2: the copy
     const uint32_t vn = wave_segments<CopyChunk>(
         (mc + 15) >> 4, lane,
@@ -927,6 +944,7 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
     const int lane = threadIdx.x & 63;
     const uint64_t t = blockIdx.x;
     if (t * 64 >= n) return;
+    ZB_STAMP(0);
     const uintptr_t fallback = (uintptr_t)&zp_safe_chunk;
     uint4* win = &lds.win[0];
     uint4* tail = &lds.win[ZP_WIN_CH * 64];
@@ -948,6 +966,7 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
         consume_group<ZP_G, T4>(i0, s.nitems, lane, va, ka, win, tail, lds.cend, s.run, t4);
     }
     wave_lds_fence();                                  // windows written by other lanes
+    ZB_STAMP(1);
     // Every lane stays to the neighbour exchange after the chains; frames
     // that are not built here are marked pending for the lane-group pass.
     const uint64_t i = t * 64 + lane;
@@ -1016,6 +1035,7 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
         err = run_chain<ZB_M_WIN>(v, (const uint8_t ZB_LDSP*)nullptr, s.shift, og, nops, wc,
                                   data, lane, &hl, &done, &hw);
     }
+    ZB_STAMP(2);
 #if ZB_LANE_PAY
     {
         // A copy that does not fit the frame failed in the chain before any
@@ -1035,6 +1055,7 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
         }
         const uint32_t delta = coop_payload(go, s.ga + s.wlen, s.ga + pe, s.ga + len, src, cB,
                                             lane);
+        ZB_STAMP(4);
         if (go) {                                      // refold the L4 checksum
             const uint32_t k4 = og.kind(nops - 1);
             const uint32_t at = k4 == ZP_B_TCP ? 16u : k4 == ZP_B_UDP ? 6u : 2u;
@@ -1104,6 +1125,7 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
                 *(ZP_GLOBAL uint8_t*)(a0 + b) = region[b];
         }
     }
+    ZB_STAMP(5);
     if (!fast) return;
     zp_build_result r;
     r.header_len = hl;

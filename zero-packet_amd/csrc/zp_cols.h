@@ -9,9 +9,27 @@
 
 #include "../../include/zero_packet.h"
 
+typedef unsigned zp_u32x2 __attribute__((ext_vector_type(2)));
+
 struct ColPtrs {
     uint8_t* p[ZP_COL_COUNT];
 };
+
+// The parse result of one frame with every field unpacked: the kernels'
+// working form, packed into the 8-B zp_record (include/zero_packet.h) only
+// at the store. final_nh / inner_final_nh are IPv6Reader::final_next_header
+// (ipv6.rs:219-227) of the outer / ip_in_ip IPv6.
+struct zp_rec_full {
+    uint32_t flags;
+    uint8_t err, eth_len, final_nh, inner_final_nh;
+    uint32_t inner_off, l4_off;
+};
+
+__device__ __forceinline__ zp_u32x2 zp_pack(const zp_rec_full& r) {
+    if (r.err) return zp_u32x2{(uint32_t)r.err << 26, 0u};
+    const uint32_t l4 = r.l4_off < ZP_L4_FAR ? r.l4_off : ZP_L4_FAR;
+    return zp_u32x2{r.flags | ((uint32_t)(r.eth_len - 14) >> 2) << 24, l4 | (r.inner_off << 18)};
+}
 
 // A reader R gives frame byte x as rd(x), and bytes [x, x + 4) as one
 // little-endian dword rd.le4(x) when rd.has4(x) (all four staged: two dword
@@ -69,7 +87,7 @@ __device__ __forceinline__ void col_mac(const ColPtrs& c, int col, uint64_t i, R
 // Writes entry i of every requested column for one frame: record r (ok =
 // parsed without error, with an Ethernet reader), frame length len.
 template <class R>
-__device__ __forceinline__ void emit_columns(R& rd, const zp_record& r, bool ok, uint32_t len,
+__device__ __forceinline__ void emit_columns(R& rd, const zp_rec_full& r, bool ok, uint32_t len,
                                              uint64_t i, const ColPtrs& c) {
     // Absent readers / errors read 0.
     uint8_t ipv = 0, proto = 0, ttl = 0, tos = 0, iv = 0, iproto = 0, l4p = 0, tflags = 0;

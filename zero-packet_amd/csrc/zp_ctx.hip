@@ -59,7 +59,7 @@ struct zp_ctx {
 // outputs between them. Frames longer than ONE_MAX take the batch path.
 #define ONE_OFFS 0       // uint64_t: ONE_FRAME
 #define ONE_LENS 8       // uint32_t
-#define ONE_REC 16       // zp_record
+#define ONE_REC 16       // zp_record (8 B)
 #define ONE_EXT 32       // zp_ext_offsets[2]
 #define ONE_FRAME 64
 #define ONE_MAX (64u << 10)
@@ -297,7 +297,7 @@ extern "C" int zp_parse_one(zp_ctx* c, const uint8_t* frame, uint64_t len,
         static const uint8_t empty[16] = {0};
         if (ext) memset(ext, 0, 2 * sizeof(zp_ext_offsets));   // unflagged entries: zero
         const int rc = zp_parse_batch_host(c, frame ? frame : empty, len, &off, &l, 1, record, ext);
-        return rc ? rc : record->err;
+        return rc ? rc : (int)zp_rec_err(*record);
     }
     hipError_t e = hipSuccess;
     {
@@ -327,7 +327,7 @@ extern "C" int zp_parse_one(zp_ctx* c, const uint8_t* frame, uint64_t len,
         if (record->flags & ZP_F_EXT) ext[0] = x[0];
         if (record->flags & ZP_F_INNER_EXT) ext[1] = x[1];
     }
-    return record->err;
+    return (int)zp_rec_err(*record);
 }
 
 // Several devices at once (one context each): the batch is cut into

@@ -82,6 +82,22 @@ struct HdrReader {
     }
 };
 
+// IPv6Reader::final_next_header (ipv6.rs:219-227) of the IPv6 header at
+// `ip`: its next-header byte, or with an extension chain the next-header
+// byte of the chain's last header (headers.rs:51-213 stops after the
+// headers the slot bits name; lengths by type as in the walk).
+template <class R>
+__device__ __forceinline__ uint32_t final_nh(R& rd, uint32_t ip, uint32_t slots) {
+    uint32_t cur = rd(ip + 6), p = ip + 40;
+    for (int k = __builtin_popcount(slots & 63u); k > 0; --k) {
+        const uint32_t b1 = rd(p + 1);
+        const uint32_t hl = cur == 44 ? 8u : cur == 51 ? (b1 + 2) * 4 : (b1 + 1) * 8;
+        cur = rd(p);
+        p += hl;
+    }
+    return cur;
+}
+
 __global__ void __launch_bounds__(FX_BLOCK)
 zp_columns_kernel(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs,
                   const uint32_t* __restrict__ lens, const zp_record* __restrict__ recs,
@@ -92,12 +108,21 @@ zp_columns_kernel(const uint8_t* __restrict__ arena, const uint64_t* __restrict_
     // early: ds_bpermute reads every lane); they load and store nothing.
     const bool live = i0 < n;
     const uint64_t i = live ? i0 : n - 1;
-    const uint4* rp = (const uint4*)(recs + i);
-    zp_record r;
+    // the 8-B record, unpacked (include/zero_packet.h); the final next
+    // headers of the IPv6 readers come from the frame after the staging
+    zp_rec_full r;
     {
-        const uint4 q = rp[0];
-        static_assert(sizeof(zp_record) == sizeof(uint4), "one 16-B load per record");
-        __builtin_memcpy(&r, &q, sizeof r);
+        static_assert(sizeof(zp_record) == 8, "one 8-B load per record");
+        const zp_u32x2 q = *(const FX_GLOBAL zp_u32x2*)(recs + i);
+        r.flags = q.x & ZP_F_MASK;
+        r.err = (uint8_t)(q.x >> 26);
+        r.eth_len = (uint8_t)(14u + 4u * ((q.x >> 24) & 3u));
+        r.final_nh = 0;
+        r.inner_final_nh = 0;
+        r.l4_off = q.y & ZP_L4_FAR;
+        r.inner_off = q.y >> 18;
+        // an L4 header past ZP_L4_FAR is not in the record: no L4 columns
+        if (r.l4_off == ZP_L4_FAR) r.flags &= ~(uint32_t)(ZP_F_TCP | ZP_F_UDP | ZP_F_ICMPV4 | ZP_F_ICMPV6);
     }
     const bool ok = live && r.err == 0 && (r.flags & ZP_F_ETHERNET);
     const uint32_t len = ok ? lens[i] : 0u;
@@ -151,6 +176,9 @@ zp_columns_kernel(const uint8_t* __restrict__ arena, const uint64_t* __restrict_
 
     if (!live) return;
     HdrReader rd{h};
+    if (ok && (r.flags & ZP_F_IPV6)) r.final_nh = (uint8_t)final_nh(rd, r.eth_len, r.flags >> 12);
+    if (ok && (r.flags & ZP_F_IP_IN_IP_V6))
+        r.inner_final_nh = (uint8_t)final_nh(rd, r.inner_off, r.flags >> 18);
     emit_columns(rd, r, ok, len, i, c);
 }
 

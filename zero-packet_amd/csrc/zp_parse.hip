@@ -375,7 +375,7 @@ __device__ __forceinline__ uint32_t wsum4n(const FrameView& f, uint32_t a, uint3
 // The header-chain walk of PacketParser::parse for one frame.
 // --------------------------------------------------------------------------
 struct Walk {
-    zp_record rec;
+    zp_rec_full rec;
     uint4 outer;             // ipv6 extension chain as a zp_ext_offsets (valid iff ZP_F_EXT)
     uint4 inner;             // ip_in_ip IPv6 chain (valid iff ZP_F_INNER_EXT)
     uint32_t acc;        // exact pseudo-header accumulator of the innermost IP
@@ -442,7 +442,7 @@ __device__ __forceinline__ int ext_walk(FrameView& f, uint32_t pos, uint32_t nh,
 }
 
 __device__ __forceinline__ void walk_frame(FrameView& f, Walk& w) {
-    zp_record& r = w.rec;
+    zp_rec_full& r = w.rec;
     w.pending = 0; w.acc = 0; w.l4 = 0; w.v6 = 0;
     const uint32_t len = f.len;
     int err = 0;
@@ -508,7 +508,8 @@ __device__ __forceinline__ void walk_frame(FrameView& f, Walk& w) {
                         r.final_nh = (uint8_t)proto;
                         if (pres) {
                             r.flags |= ZP_F_EXT | (pres << 12);
-                            w.outer = make_uint4(eo[0] | tot, eo[1], eo[2], eo[3]);
+                            // final_next_header (headers.rs:26) in byte 14
+                            w.outer = make_uint4(eo[0] | tot, eo[1], eo[2], eo[3] | (proto << 16));
                         }
                     } else if (level == 1) {
                         r.flags |= ZP_F_IP_IN_IP | ZP_F_IP_IN_IP_V6;
@@ -516,7 +517,7 @@ __device__ __forceinline__ void walk_frame(FrameView& f, Walk& w) {
                         r.inner_final_nh = (uint8_t)proto;
                         if (pres) {
                             r.flags |= ZP_F_INNER_EXT | (pres << 18);
-                            w.inner = make_uint4(eo[0] | tot, eo[1], eo[2], eo[3]);
+                            w.inner = make_uint4(eo[0] | tot, eo[1], eo[2], eo[3] | (proto << 16));
                         }
                     }
                 }
@@ -582,7 +583,7 @@ __device__ __forceinline__ void walk_frame(FrameView& f, Walk& w) {
     }
 done:
     if (err) {
-        r = zp_record{};
+        r = zp_rec_full{};
         r.err = (uint8_t)err;
         w.pending = 0;
     }
@@ -729,7 +730,7 @@ __device__ __forceinline__ bool fast_ip(FrameView& f, Walk& w) {
                      : icmpv6_type_ok(t >> 8);                             // parser.rs:293-299
         }
     }
-    zp_record& r = w.rec;
+    zp_rec_full& r = w.rec;
     r.flags = ZP_F_ETHERNET | (v4o ? ZP_F_IPV4 : ZP_F_IPV6) |
               (enc ? ZP_F_IP_IN_IP | (v4i ? 0u : ZP_F_IP_IN_IP_V6) : 0u) |
               (tcp ? ZP_F_TCP : udp ? ZP_F_UDP : ic4 ? ZP_F_ICMPV4 : ic6 ? ZP_F_ICMPV6 : 0u);
@@ -811,14 +812,9 @@ __device__ __forceinline__ bool tiny_tile(uint64_t tile, uint32_t len, uintptr_t
     ok = ok && csum_ok(acc, lv, false);
     if (__ballot(live && !ok)) return false;                           // wave-uniform
     if (live) {
-        zp_record rec{};
-        rec.flags = ZP_F_ETHERNET | ZP_F_IPV4 | (tcp ? ZP_F_TCP : udp ? ZP_F_UDP : ZP_F_ICMPV4);
-        rec.eth_len = 14;
-        rec.l4_off = 34;
-        uint4 q;
-        memcpy(&q, &rec, sizeof rec);
-        __builtin_nontemporal_store(zp_u32x4{q.x, q.y, q.z, q.w},
-                                    (zp_u32x4*)(records + tile * 64 + lane));
+        // Ethernet II (code 0), IPv4, the L4 reader at 34
+        const uint32_t flags = ZP_F_ETHERNET | ZP_F_IPV4 | (tcp ? ZP_F_TCP : udp ? ZP_F_UDP : ZP_F_ICMPV4);
+        __builtin_nontemporal_store(zp_u32x2{flags, 34u}, (zp_u32x2*)(records + tile * 64 + lane));
     }
     return true;
 }
@@ -855,7 +851,7 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
     fv.xc = make_uint4(0, 0, 0, 0);
     fv.xi = ~0u;
     Walk w;
-    w.rec = zp_record{};
+    w.rec = zp_rec_full{};
     w.outer = make_uint4(0, 0, 0, 0);
     w.inner = make_uint4(0, 0, 0, 0);
 #ifdef ZP_ABL_FAKE_WALK
@@ -884,7 +880,7 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
 #endif
     if (__ballot(s.live && !done)) {
         if (s.live && !done) {
-            w.rec = zp_record{};
+            w.rec = zp_rec_full{};
             walk_frame(fv, w);
         }
     }
@@ -893,7 +889,7 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
     if (!s.live) return;
     // The frame's stream sum covers the whole chunks [A & ~15, E16):
     // L4 sum = that - V[A & ~15, A + l4) - V[E, E16).
-    zp_record rec = w.rec;
+    zp_rec_full rec = w.rec;
     if (w.pending) {
         bool ok;
         if (s.giant) {
@@ -911,26 +907,24 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
 #endif
         }
         if (!ok) {
-            rec = zp_record{};
+            rec = zp_rec_full{};
             rec.err = (uint8_t)(w.v6 ? ZP_ERR_IPV6_L4_CHECKSUM : ZP_ERR_IPV4_L4_CHECKSUM);
         }
     }
     STAMP(6);
-    static_assert(sizeof(zp_record) == 16 && sizeof(zp_ext_offsets) == 16, "16-B records");
+    static_assert(sizeof(zp_record) == 8 && sizeof(zp_ext_offsets) == 16, "8-B records");
     const uint64_t p = s.tile * 64 + lane;
 #ifdef ZP_ABL_NOREC
     if (rec.flags == 0xDEADBEEFu)                       // timing ablation: no stores
 #endif
     {
-        // One nontemporal 16-B store per frame: 1 KiB of whole lines per wave
-        // instruction. The record writes, not their share of the bytes, are
-        // what makes the kernel sensitive to the placement of the arena and
-        // the records (without them every placement runs in 1.95 ms); nt took
-        // 6-7 % off on every placement, and 16-B records (v2) 4-6 % more
-        // than 32-B ones.
-        uint4 q;
-        memcpy(&q, &rec, sizeof rec);
-        __builtin_nontemporal_store(zp_u32x4{q.x, q.y, q.z, q.w}, (zp_u32x4*)(records + p));
+        // One nontemporal 8-B store per frame: 512 B of whole lines per wave
+        // instruction. Writes mixed into the read stream cost several times
+        // their bytes and make the kernel sensitive to the placement of the
+        // arena and the records: nt took 6-7 % off on every
+        // placement, 16-B records (v2) 4-6 % against 32-B ones, and 8-B
+        // records (v4) 2-7 % more.
+        __builtin_nontemporal_store(zp_pack(rec), (zp_u32x2*)(records + p));
     }
     if (ext) {
         // The extension chains: a wave with at least ZP_EXT_DENSE chains

@@ -104,6 +104,7 @@ static int ext_walk(const uint8_t* p, uint64_t n, uint8_t nh, zp_reader_info* in
         for (int k = 0; k < ZP_EXT_SLOTS; ++k)
             if (have & (1u << k)) info->flags |= ZP_F_EXT_SLOT(k);
         info->ext.len = (uint16_t)total;
+        info->ext.final_nh = final_nh;                           /* headers.rs:26 */
         info->final_nh = final_nh;
     }
     return ZP_OK;

@@ -9,7 +9,7 @@
 // into a device array of ZP_STATS_COUNT u64. A multi-GPU job sums its ranks'
 // arrays on the host: the frames are independent, there is no exchange step.
 //
-// HBM-bound on the 16-B records: one dwordx4 load per frame, lane-parallel
+// HBM-bound on the 8-B records: one dwordx2 load per frame, lane-parallel
 // (SWAR) flag counts, one set of u64 atomics per workgroup.
 
 #include <hip/hip_runtime.h>
@@ -23,14 +23,14 @@ extern "C" char* zp__errbuf(void);
 #define ST_BLOCK 256
 #define ST_WAVES (ST_BLOCK / 64)
 #ifndef ST_U
-#define ST_U 4                     // records per lane in flight
+#define ST_U 8                     // records per lane in flight (4 KiB per wave)
 #endif
 #ifndef ST_GRID
 #define ST_GRID 512                // workgroups at most: 2 per CU, each looping over its
 #endif                             // share (2048: 63 us per 16M records, 512: 48 us; the
                                    // per-workgroup atomics contend)
 #define ST_GLOBAL __attribute__((address_space(1)))
-typedef unsigned st_u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned st_u32x2 __attribute__((ext_vector_type(2)));
 
 // Lane-parallel counting: bit b of a record's flags is counted in byte b / 8
 // of acc[b % 8] (SWAR, four counters per register), so a record costs eight
@@ -57,20 +57,20 @@ zp_stats_kernel(const zp_record* __restrict__ recs, uint64_t n,
     const uint64_t stride = (uint64_t)gridDim.x * ST_BLOCK;
     for (uint64_t i0 = (uint64_t)blockIdx.x * ST_BLOCK + threadIdx.x; i0 - lane < n;
          i0 += ST_U * stride) {
-        // ST_U records per lane in flight per trip (coalesced 1 KiB wave loads)
-        st_u32x4 q[ST_U];
+        // ST_U records per lane in flight per trip (coalesced 512-B wave loads)
+        st_u32x2 q[ST_U];
 #pragma unroll
         for (int u = 0; u < ST_U; ++u) {
             const uint64_t i = i0 + u * stride;
             q[u] = __builtin_nontemporal_load(
-                (const ST_GLOBAL st_u32x4*)(recs + (i < n ? i : n - 1)));
+                (const ST_GLOBAL st_u32x2*)(recs + (i < n ? i : n - 1)));
         }
 #pragma unroll
         for (int u = 0; u < ST_U; ++u) {
             const uint64_t i = i0 + u * stride;
             const bool live = i < n;
-            const uint32_t flags = live ? q[u].x : 0u;
-            const uint32_t err = q[u].y & 0xFFu;    // zp_record: flags, then err at byte 4
+            const uint32_t flags = live ? q[u].x & ZP_F_MASK : 0u;
+            const uint32_t err = q[u].x >> 26;       // zp_record: err in flags bits 26-31
 #pragma unroll
             for (int j = 0; j < 8; ++j) acc[j] += (flags >> j) & 0x01010101u;
             const uint64_t ok = __ballot(live && err == 0);

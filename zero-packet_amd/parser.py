@@ -481,15 +481,16 @@ class PacketParser:
         ip_in_ip chain; EXT_DTYPE [2]), needed when the record flags a chain.
         Raises ZeroPacketError when the record holds an error."""
         frame = bytes(frame)
-        err = int(rec["err"])
+        word, offs = int(rec["flags"]), int(rec["offs"])
+        err = word >> 26
         if err:
             raise ZeroPacketError(_lib.hip().zp_err_str(err).decode() if _lib_available()
                                   else f"zp_err {err}", err)
-        flags = int(rec["flags"])
+        flags = word & _rec.F_MASK
         if flags & (F_EXT | F_INNER_EXT) and ext is None:
             raise ValueError("the record flags an IPv6 extension chain: pass its ext entries")
         p = cls()
-        hl = int(rec["eth_len"])
+        hl = 14 + 4 * ((word >> 24) & 3)
         if flags & F_ETHERNET:
             p.ethernet = EthernetReader(frame, hl)
         if flags & F_ARP:
@@ -500,21 +501,23 @@ class PacketParser:
             eh = None
             if flags & F_EXT:
                 x = ext[0]
-                eh = _ext_from(frame, hl + 40, flags, 12, x["off"], x["len"], rec["final_nh"])
+                eh = _ext_from(frame, hl + 40, flags, 12, x["off"], x["len"], x["final_nh"])
             p.ipv6 = IPv6Reader(frame[hl:], eh, int(ext[0]["len"]) if eh else 0)
         if flags & F_IP_IN_IP:
-            io = int(rec["inner_off"])
+            io = offs >> 18
             if flags & F_IP_IN_IP_V6:
                 eh = None
                 if flags & F_INNER_EXT:
                     x = ext[1]
-                    eh = _ext_from(frame, io + 40, flags, 18, x["off"], x["len"],
-                                   rec["inner_final_nh"])
+                    eh = _ext_from(frame, io + 40, flags, 18, x["off"], x["len"], x["final_nh"])
                 p.ip_in_ip = IpInIp("ipv6", IPv6Reader(frame[io:], eh,
                                                        int(ext[1]["len"]) if eh else 0))
             else:
                 p.ip_in_ip = IpInIp("ipv4", IPv4Reader(frame[io:]))
-        l4 = int(rec["l4_off"])
+        l4 = offs & _rec.L4_FAR
+        if l4 == _rec.L4_FAR and flags & (F_TCP | F_UDP | F_ICMPV4 | F_ICMPV6):
+            raise ValueError("the L4 header starts at or past ZP_L4_FAR (262,143): "
+                             "not representable in the 8-B record")
         if flags & F_TCP:
             p.tcp = TcpReader(frame[l4:])
         if flags & F_UDP:

@@ -1,17 +1,47 @@
-"""zp_record layout (include/zero_packet.h) as a numpy structured dtype."""
+"""zp_record layout (include/zero_packet.h, ABI v4) as numpy dtypes."""
 import numpy as np
 
-RECORD_DTYPE = np.dtype([
-    ("flags", "<u4"), ("err", "u1"), ("eth_len", "u1"), ("final_nh", "u1"),
-    ("inner_final_nh", "u1"), ("inner_off", "<u4"), ("l4_off", "<u4"),
-])
-assert RECORD_DTYPE.itemsize == 16
+# The 8-B record: flags (bits 0-23 ZP_F_*, 24-25 Ethernet code, 26-31 err)
+# and offs (bits 0-17 l4_off, 18-31 inner_off). unpack() gives the fields.
+RECORD_DTYPE = np.dtype([("flags", "<u4"), ("offs", "<u4")])
+assert RECORD_DTYPE.itemsize == 8
+# unpack()'s per-field view (the final next headers are not in the record:
+# ext entry of a chain, else the IPv6 next-header byte)
+FIELDS_DTYPE = np.dtype([("flags", "<u4"), ("err", "u1"), ("eth_len", "u1"),
+                         ("inner_off", "<u4"), ("l4_off", "<u4")])
+F_MASK = 0x00FFFFFF
+L4_FAR = 0x3FFFF          # ZP_L4_FAR: an L4 header at or past this offset
 # One IPv6 extension chain (zp_ext_offsets). A batch of n frames has 2n of
 # them: [0, n) the outer ipv6 chains, [n, 2n) the ip_in_ip ones; numpy views
-# them as shape (2, n).
-EXT_DTYPE = np.dtype([("len", "<u2"), ("off", "<u2", (6,)), ("reserved", "<u2")])
+# them as shape (2, n). final_nh = ExtensionHeaders::final_next_header.
+EXT_DTYPE = np.dtype([("len", "<u2"), ("off", "<u2", (6,)), ("final_nh", "u1"),
+                      ("reserved", "u1")])
 assert EXT_DTYPE.itemsize == 16
-RECORD_BYTES, EXT_BYTES = 16, 16
+RECORD_BYTES, EXT_BYTES = 8, 16
+
+
+def unpack(rec):
+    """RECORD_DTYPE array (or raw uint8 [n, 8]) -> FIELDS_DTYPE array."""
+    rec = np.asarray(rec)
+    if rec.dtype != RECORD_DTYPE:
+        rec = np.ascontiguousarray(rec, dtype=np.uint8).view(RECORD_DTYPE).reshape(-1)
+    w, o = rec["flags"].astype(np.uint32), rec["offs"].astype(np.uint32)
+    out = np.zeros(w.shape, FIELDS_DTYPE)
+    err = w >> 26
+    out["err"] = err
+    ok = err == 0
+    out["flags"] = np.where(ok, w & F_MASK, 0)
+    out["eth_len"] = np.where(ok, 14 + 4 * ((w >> 24) & 3), 0)
+    out["l4_off"] = np.where(ok, o & L4_FAR, 0)
+    out["inner_off"] = np.where(ok, o >> 18, 0)
+    return out
+
+
+def rec_err(rec):
+    """err codes of RECORD_DTYPE records (array or scalar)."""
+    return np.asarray(rec["flags"]).astype(np.uint32) >> 26
+
+
 # zp_reader_info (zp_reader_new): Ethernet header_len; IPv6 chain bits,
 # final_next_header and offsets.
 READER_INFO_DTYPE = np.dtype([("header_len", "<u4"), ("flags", "<u4"), ("final_nh", "u1"),
