@@ -35,7 +35,7 @@ def main():
         frecs, _, fcols = zp.columns.parse_with_columns(a, o, l_)
         torch.cuda.synchronize()
         assert torch.equal(frecs, recs), f"round {r}: fused records differ"
-        want = orc.columns(arena, offs, lens, zp.batch.records_to_numpy(recs))
+        want = orc.columns(arena, offs, lens, orc.parse_batch(arena, offs, lens)[0])
         for name in zp.columns.NAMES:
             assert np.array_equal(got[name].cpu().numpy(), want[name]), (r, name)
             assert np.array_equal(fcols[name].cpu().numpy(), want[name]), (r, "fused", name)

@@ -123,7 +123,20 @@ def main():
                 nbytes = buf.numel() // region * region
                 print(f"tiles {label:24s} records={(0, 16, 8)[rec]}B: {np.median(ms):.3f} ms "
                       f"{nbytes / (np.median(ms) * 1e-3) / 1e9:.0f} GB/s", flush=True)
-        del buf, out
+        del out
+        # the copy pattern (builder payload pass): read + write the same bytes
+        mb.membw_copy_tiles.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                        ctypes.c_uint64, ctypes.c_void_p]
+        half = (6 << 30)
+        dst = torch.empty(half, dtype=torch.uint8, device=dev)
+        for label, region in (("c3 tile", 50016), ("c5 tile", 22672)):
+            ms = time_launches(lambda: mb.membw_copy_tiles(buf.data_ptr(), dst.data_ptr(), half,
+                                                           region, None), 10)
+            nbytes = half // region * region
+            print(f"copy tiles {label:16s}: {np.median(ms):.3f} ms read {nbytes / 1e9:.2f} GB + "
+                  f"write {nbytes / 1e9:.2f} GB = {2 * nbytes / (np.median(ms) * 1e-3) / 1e9:.0f} GB/s",
+                  flush=True)
+        del buf, dst
         torch.cuda.empty_cache()
     if args.c2cold:
         n = 1 << 20

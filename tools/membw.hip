@@ -235,3 +235,37 @@ extern "C" int membw_tiles(const void* p, uint64_t bytes, uint32_t* out, uint64_
                             (const uint8_t*)p, region, nreg, out, lds_bytes);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+
+// Copy pattern of the builder's payload pass: one wave per tile-sized region,
+// 1 KiB nontemporal loads in groups of 8 from src, the same bytes stored to
+// dst with plain 16-B stores (whole lines; no LDS).
+__global__ void __launch_bounds__(64) copy_tiles(const uint8_t* __restrict__ src,
+                                                 uint8_t* __restrict__ dst, uint64_t region) {
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    const int lane = threadIdx.x;
+    const uint64_t w = blockIdx.x;
+    const uint64_t nch = region / 16, items = (nch + 63) / 64;
+    for (uint64_t i = 0; i < items; i += 8) {
+        u32x4 v[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            uint64_t c = (i + q) * 64 + lane;
+            c = c < nch ? c : nch - 1;
+            v[q] = __builtin_nontemporal_load(
+                (const __attribute__((address_space(1))) u32x4*)(src + w * region + c * 16));
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const uint64_t c = (i + q) * 64 + lane;
+            if (c < nch) *(u32x4*)(dst + w * region + c * 16) = v[q];
+        }
+    }
+}
+
+extern "C" int membw_copy_tiles(const void* src, void* dst, uint64_t bytes, uint64_t region,
+                                void* stream) {
+    const uint64_t nreg = bytes / region;
+    hipLaunchKernelGGL(copy_tiles, dim3((unsigned)nreg), dim3(64), 0, (hipStream_t)stream,
+                       (const uint8_t*)src, (uint8_t*)dst, region);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
