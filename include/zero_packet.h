@@ -117,7 +117,7 @@ typedef enum zp_err {
  * One parse result, 8 bytes (one dwordx2 store per frame). The record writes
  * are the only HBM writes of the parse, and writes mixed into the read
  * stream cost several times their bytes: the 8-B record took
- * 3-7 % off every configuration against the 16-B record of ABI v2/v3.
+ * 2-7 % off every configuration against the 16-B record of ABI v2/v3.
  *
  *   flags  bits  0-23  ZP_F_* presence and extension-slot bits (above)
  *          bits 24-25  Ethernet header length: 14 + 4 * code (14 / 18 / 22,

@@ -3,7 +3,7 @@
     arena  uint8  [B]       frames packed anywhere in one buffer
     offs   int64  [n]       frame start offsets (read as uint64)
     lens   int32  [n]       frame lengths (read as uint32)
-    -> records uint8 [n, 16] (zp_record), ext uint8 [2, n, 16] (zp_ext_offsets:
+    -> records uint8 [n, 8] (zp_record), ext uint8 [2, n, 16] (zp_ext_offsets:
        [0] the outer ipv6 extension chains, [1] the ip_in_ip ones; an entry
        is valid where the record's ZP_F_EXT / ZP_F_INNER_EXT bit is set)
 
@@ -82,7 +82,7 @@ def check_batch(arena, offs, lens, outs=(), bounds=True, stream=None):
 
 
 def alloc_outputs(n, device, records=None, ext=None):
-    """records uint8 [n, 16] and ext uint8 [2, n, 16] device tensors (the ones
+    """records uint8 [n, 8] and ext uint8 [2, n, 16] device tensors (the ones
     given are kept)."""
     if records is None:
         records = torch.empty((n, RECORD_BYTES), dtype=torch.uint8, device=device)

@@ -15,7 +15,7 @@
 //      and cut into items of 64 chunks; see "The stream" below); per-frame
 //      sums by running prefix; header windows and last chunks to LDS;
 //   3. lane-per-frame header walk from the LDS window;
-//   4. checksum verdict, 16-B record store (+ extension chains, if any).
+//   4. checksum verdict, 8-B record store (+ extension chains, if any).
 // Checksum arithmetic. The reference verifies S = acc + sum of big-endian
 // 16-bit words (u32), valid iff !fold(S) as u16 == 0 (checksum.rs:5-35),
 // i.e. S != 0 and S == 0 (mod 65535). We sum little-endian 16-bit words at

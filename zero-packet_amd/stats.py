@@ -27,13 +27,13 @@ assert len(FLAG_NAMES) == FLAG_BITS
 
 
 def count(records, counts=None, stream=None):
-    """Adds the counts of `records` (uint8 [n, 16] device tensor) into
+    """Adds the counts of `records` (uint8 [n, 8] device tensor) into
     `counts` (int64 [COUNT] device tensor, zeroed when not given)."""
     if not records.is_cuda:
         raise RuntimeError("stats.count needs device records (no CPU fallback)")
     if (records.dtype != torch.uint8 or records.dim() != 2 or records.shape[1] != RECORD_BYTES
             or not records.is_contiguous()):
-        raise ValueError("records must be a contiguous uint8 [n, 16] tensor")
+        raise ValueError(f"records must be a contiguous uint8 [n, {RECORD_BYTES}] tensor")
     if counts is None:
         counts = torch.zeros(COUNT, dtype=torch.int64, device=records.device)
     if (counts.numel() != COUNT or counts.dtype != torch.int64 or counts.device != records.device
