@@ -779,6 +779,9 @@ __device__ __forceinline__ uint32_t chain_extent(const OpGlobal& ops, uint32_t n
 #ifndef ZB_LANE_PAY
 #define ZB_LANE_PAY 1          // payload copies past the window on the lane path
 #endif
+#ifndef ZB_WIDE_EDGES
+#define ZB_WIDE_EDGES 1        // partial 16-B chunks by dword/short/byte stores (0: byte loop)
+#endif
 
 // Diagnostic build only (-DZB_STAMPS, tools/build_bench.py --stamps): per-wave
 // s_memrealtime stamps at the phase boundaries of zp_build_fast_kernel.
@@ -845,6 +848,45 @@ __device__ __forceinline__ uint32_t wave_segments(uint32_t cnt, int lane, L&& lo
 
 __device__ __forceinline__ uint64_t bperm64(uint64_t v, uint32_t r) {
     return ((uint64_t)bperm((uint32_t)(v >> 32), r) << 32) | bperm((uint32_t)v, r);
+}
+
+// Bytes [s, e) of the 16-B chunk q to the 16-B-aligned address X (0 <= s <
+// e <= 16) in at most one byte, one short, one 1-4 dword and one short + byte
+// store per lane, instead of one byte store per byte: a wave whose lanes end
+// their ranges anywhere in a chunk issues a handful of store instructions, not
+// up to 15 (ZB_WIDE_EDGES).
+__device__ __forceinline__ uint32_t q_dw(uint4 q, uint32_t i) {
+    return i == 0 ? q.x : i == 1 ? q.y : i == 2 ? q.z : q.w;
+}
+__device__ __forceinline__ void store_bytes(uintptr_t X, uint4 q, uint32_t s, uint32_t e) {
+    uint32_t b = s;
+    if ((b & 1u) && b < e) {
+        *(ZP_GLOBAL uint8_t*)(X + b) = (uint8_t)(q_dw(q, b >> 2) >> (8 * (b & 3u)));
+        ++b;
+    }
+    if ((b & 2u) && b + 2 <= e) {
+        *(ZP_GLOBAL uint16_t*)(X + b) = (uint16_t)(q_dw(q, b >> 2) >> 16);
+        b += 2;
+    }
+    const uint32_t nd = (b & 3u) == 0 && b < e ? (e - b) >> 2 : 0u;
+    if (nd) {
+        const uint32_t i = b >> 2;
+        const uint32_t d0 = q_dw(q, i), d1 = q_dw(q, i + 1), d2 = q_dw(q, i + 2);
+        if (nd == 1) *(ZP_GLOBAL uint32_t*)(X + b) = d0;
+        else if (nd == 2) *(ZP_GLOBAL zp_u32x2*)(X + b) = zp_u32x2{d0, d1};
+        else if (nd == 3) {
+            typedef unsigned u32x3 __attribute__((ext_vector_type(3)));
+            *(ZP_GLOBAL u32x3*)(X + b) = u32x3{d0, d1, d2};
+        } else {
+            *(ZP_GLOBAL zp_u32x4*)(X + b) = zp_u32x4{q.x, q.y, q.z, q.w};
+        }
+        b += 4 * nd;
+    }
+    if (b + 2 <= e) {                                  // b is 4-aligned here
+        *(ZP_GLOBAL uint16_t*)(X + b) = (uint16_t)q_dw(q, b >> 2);
+        b += 2;
+    }
+    if (b < e) *(ZP_GLOBAL uint8_t*)(X + b) = (uint8_t)(q_dw(q, b >> 2) >> (8 * (b & 3u)));
 }
 
 struct CopyChunk { uint32_t x[5]; uintptr_t X; uint32_t m, sh; };
@@ -917,9 +959,13 @@ __device__ __forceinline__ uint32_t coop_payload(bool go, uintptr_t D0, uintptr_
             if (c.m == 16) {
                 *(ZP_GLOBAL zp_u32x4*)c.X = zp_u32x4{q.x, q.y, q.z, q.w};
             } else {
+#if ZB_WIDE_EDGES
+                store_bytes(c.X, q, 0, c.m);
+#else
                 const uint32_t w[4] = {q.x, q.y, q.z, q.w};
                 for (uint32_t b = 0; b < c.m; ++b)
                     *(ZP_GLOBAL uint8_t*)(c.X + b) = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
+#endif
             }
             return range_sum(q, 0, c.m);
         });
@@ -1121,8 +1167,13 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
             const uint4 q = ld_region(region, lo);
             *(ZP_GLOBAL zp_u32x4*)(a0 + lo) = zp_u32x4{q.x, q.y, q.z, q.w};
         } else {
+#if ZB_WIDE_EDGES
+            const uint32_t bs = lo < sh ? sh : lo, be = hi < end ? hi : end;
+            if (bs < be) store_bytes(a0 + lo, ld_region(region, lo), bs - lo, be - lo);
+#else
             for (uint32_t b = lo < sh ? sh : lo; b < (hi < end ? hi : end); ++b)
                 *(ZP_GLOBAL uint8_t*)(a0 + b) = region[b];
+#endif
         }
     }
     ZB_STAMP(5);
