@@ -809,16 +809,20 @@ extern "C" int zb_stamps_set(void* p) {
 // wrapping sum of its own chunks' contributions (running-sum differences:
 // no segmented reduction). Every lane must be active (DPP scans, bpermute).
 #ifndef ZB_COOP_U
-#define ZB_COOP_U 2            // 1: 2.04 / 3.52 ms, 2: 1.95 / 3.16, 4: 1.99 / 3.26, 8: 2.11 / 3.52 (P = 200 / 1000)
+#define ZB_COOP_U 4            // without ZB_PIPE_SEARCH 1: 2.04 / 3.52 ms, 2: 1.95 / 3.16, 4: 1.99 / 3.26, 8: 2.11 / 3.52 (P = 200 / 1000); with it 2: 1.85 / 2.80, 4: 1.82 / 2.71, 8: 1.82 / 2.70
+#endif
+// ZB_PIPE_SEARCH: the owner search of the next ZB_COOP_U items (dependent
+// ds_bpermute round trips) is issued while this round's loads are in flight,
+// not after its stores.
+#ifndef ZB_PIPE_SEARCH
+#define ZB_PIPE_SEARCH 1
 #endif
 template <class D, class L, class U>
 __device__ __forceinline__ uint32_t wave_segments(uint32_t cnt, int lane, L&& load, U&& use) {
     const uint32_t incl = wave_scan(cnt), pre = incl - cnt;
     const uint32_t T = rdl(incl, 63);
     uint32_t carry = 0, p_pre = 0, p_end = 0;
-    for (uint32_t base = 0; base < T; base += 64 * ZB_COOP_U) {
-        uint32_t jj[ZB_COOP_U], kk[ZB_COOP_U];
-        D d[ZB_COOP_U];
+    auto search = [&](uint32_t base, uint32_t* jj, uint32_t* kk) {
 #pragma unroll
         for (int u = 0; u < ZB_COOP_U; ++u) {
             const uint32_t g = base + 64u * u + (uint32_t)lane;
@@ -828,12 +832,30 @@ __device__ __forceinline__ uint32_t wave_segments(uint32_t cnt, int lane, L&& lo
                 j = bperm(pre, j + st) <= g ? j + st : j;
             jj[u] = j;
             kk[u] = g - bperm(pre, j);
-            d[u] = load(j, kk[u], g < T);
         }
+    };
+    uint32_t jj[ZB_COOP_U], kk[ZB_COOP_U];
+#if ZB_PIPE_SEARCH
+    if (T) search(0, jj, kk);
+#endif
+    for (uint32_t base = 0; base < T; base += 64 * ZB_COOP_U) {
+        D d[ZB_COOP_U];
+#if !ZB_PIPE_SEARCH
+        search(base, jj, kk);
+#endif
+#pragma unroll
+        for (int u = 0; u < ZB_COOP_U; ++u)
+            d[u] = load(jj[u], kk[u], base + 64u * u + (uint32_t)lane < T);
+        uint32_t ju[ZB_COOP_U], ku[ZB_COOP_U];
+#pragma unroll
+        for (int u = 0; u < ZB_COOP_U; ++u) ju[u] = jj[u], ku[u] = kk[u];
+#if ZB_PIPE_SEARCH
+        if (base + 64 * ZB_COOP_U < T) search(base + 64 * ZB_COOP_U, jj, kk);
+#endif
 #pragma unroll
         for (int u = 0; u < ZB_COOP_U; ++u) {
             const uint32_t b = base + 64u * u;
-            const uint32_t v = use(d[u], jj[u], kk[u], b + (uint32_t)lane < T);
+            const uint32_t v = use(d[u], ju[u], ku[u], b + (uint32_t)lane < T);
             const uint32_t inc = wave_scan(v), exc = inc - v;
             const uint32_t xp = bperm(exc, (pre - b) & 63u), xe = bperm(exc, (incl - b) & 63u);
             if (pre >= b && pre < b + 64) p_pre = carry + xp;
