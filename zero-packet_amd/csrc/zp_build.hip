@@ -302,6 +302,9 @@ struct NoWin {
 // Executes one chain (all checks of the reference, in its order). Returns
 // the zp_build_err; *hl_out = header_len after the last Ok op, *hw_out = an
 // upper bound of the bytes written ([0, hw)).
+#ifndef ZB_OP_NEXT
+#define ZB_OP_NEXT 0
+#endif
 template <int MODE, typename P, typename OPS, typename WC>
 __device__ int run_chain(BView<P>& v, const uint8_t ZB_LDSP* stage, uint32_t shift,
                          const OPS& ops, uint32_t nops, const WC& wc,
@@ -316,8 +319,17 @@ __device__ int run_chain(BView<P>& v, const uint8_t ZB_LDSP* stage, uint32_t shi
     st = BS_RAW;
     uint32_t hl = 0, hw = 0;
     const uint32_t n = v.n;
+#if ZB_OP_NEXT
+    zp_build_op nxt{};
+    if (nops) nxt = ops.get(0);                      // an empty chain loads nothing
+#endif
     for (uint32_t k = 0; k < nops; ++k) {
+#if ZB_OP_NEXT
+        const zp_build_op o = nxt;                   // op k+1's load overlaps op k
+        if (k + 1 < nops) nxt = ops.get(k + 1);
+#else
         const zp_build_op o = ops.get(k);
+#endif
         const int prev = st;
         st = bnext(st, o.kind);
         const bool has = o.data_len != ZP_BUILD_NO_DATA;
@@ -661,7 +673,42 @@ struct OpGlobal {
     __device__ __forceinline__ uint32_t kind(uint32_t k) const {
         return *(const ZP_GLOBAL uint8_t*)(g + k);
     }
+    // what chain_extent needs of op k: bytes 0-3 (kind, b[0], b[1]) and data_len
+    __device__ __forceinline__ uint2 head(uint32_t k) const {
+        const ZP_GLOBAL uint32_t* q = (const ZP_GLOBAL uint32_t*)(g + k);
+        return make_uint2(q[0], q[7]);
+    }
 };
+
+// ZB_OP_PREFETCH: the heads of a chain's first ZB_OPH ops are loaded before
+// the stream (their latency hides behind it), chain_extent reads them from
+// registers after it; later ops are loaded then.
+#ifndef ZB_OP_PREFETCH
+#define ZB_OP_PREFETCH 1
+#endif
+#define ZB_OPH 4
+struct OpHeads {
+    OpGlobal og;
+    uint2 h[ZB_OPH];
+    __device__ __forceinline__ void load(uint32_t nops) {
+#pragma unroll
+        for (uint32_t k = 0; k < ZB_OPH; ++k) h[k] = k < nops ? og.head(k) : make_uint2(0, 0);
+    }
+    __device__ __forceinline__ uint2 head(uint32_t k) const {
+        uint2 r = make_uint2(0, 0);
+#pragma unroll
+        for (uint32_t j = 0; j < ZB_OPH; ++j) if (k == j) r = h[j];
+        return k < ZB_OPH ? r : og.head(k);
+    }
+    // run_chain's accessors: kinds from the heads, whole ops from HBM
+    __device__ __forceinline__ zp_build_op get(uint32_t k) const { return og.get(k); }
+    __device__ __forceinline__ uint32_t kind(uint32_t k) const {
+        return k < ZB_OPH ? (head(k).x & 0xFFu) : og.kind(k);
+    }
+};
+#ifndef ZB_OP_KINDS
+#define ZB_OP_KINDS 0          // run_chain's typestate pass reads the prefetched kinds
+#endif
 
 __device__ __forceinline__ uint32_t sad4(uint4 q) {
     return sad16(q.w, sad16(q.z, sad16(q.y, sad16(q.x, 0u))));
@@ -730,14 +777,20 @@ struct WinCsum {
 // Upper bound of the bytes a chain can read or write (from its ops alone;
 // the offsets the writers derive from the buffer are the values the chain
 // itself wrote: ihl, data offset, extension lengths).
-__device__ __forceinline__ uint32_t chain_extent(const OpGlobal& ops, uint32_t nops, uint32_t* pay_at = nullptr,
+template <class Ops>
+__device__ __forceinline__ uint32_t chain_extent(const Ops& ops, uint32_t nops, uint32_t* pay_at = nullptr,
                              uint32_t* pay_len = nullptr) {
     // With pay_at: the final L4 op's payload copy is left out of the extent
     // and reported as [*pay_at, *pay_at + *pay_len) (frame offsets).
     uint32_t hl = 0, top = 0;
     if (pay_at) { *pay_at = 0; *pay_len = 0; }
     for (uint32_t k = 0; k < nops; ++k) {
-        const zp_build_op o = ops.get(k);
+        const uint2 hd = ops.head(k);
+        struct { uint32_t kind; uint8_t b[2]; uint32_t data_len; } o;
+        o.kind = hd.x & 0xFFu;
+        o.b[0] = (uint8_t)(hd.x >> 8);
+        o.b[1] = (uint8_t)(hd.x >> 16);
+        o.data_len = hd.y;
         const uint32_t dl = o.data_len != ZP_BUILD_NO_DATA ? o.data_len : 0u;
         uint32_t ext = 0, adv = 0;
         switch (o.kind) {
@@ -1025,6 +1078,10 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
     load_desc(arena, offs, lens, n, t, lane, len, ga);
     TileState s;
     tile_setup(s, t, len, ga, n, lane, lds);
+#if ZB_OP_PREFETCH && ZB_LANE_PAY
+    OpHeads oh{OpGlobal{ops + (ip < n ? pf0 : 0u)}};
+    oh.load(ip < n && pf1 >= pf0 ? pf1 - pf0 : 0u);
+#endif
     uint4 va[ZP_G];
     uint32_t ka[ZP_G];
     issue_group<ZP_G, T4>(0, s.nitems, s.cur, s.R, lane, fallback, va, ka);
@@ -1050,7 +1107,11 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
         // A final payload copy may reach past the window: the headers must
         // fit it; the copy's bytes past it go straight to HBM after the chain.
         if (o1 >= o0 && len >= 64 && !s.giant) {
+#if ZB_OP_PREFETCH
+            fast = chain_extent(oh, nops, &pay_at, &pay_len) <= s.wlen;
+#else
             fast = chain_extent(OpGlobal{ops + o0}, nops, &pay_at, &pay_len) <= s.wlen;
+#endif
             pay = fast && pay_len && pay_at + pay_len > s.wlen;
         }
 #else
@@ -1100,7 +1161,11 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
         // checksum is refolded with that copy's V change below.
         if (pay) v.lim = s.wlen;
 #endif
+#if ZB_OP_PREFETCH && ZB_OP_KINDS && ZB_LANE_PAY
+        err = run_chain<ZB_M_WIN>(v, (const uint8_t ZB_LDSP*)nullptr, s.shift, oh, nops, wc,
+#else
         err = run_chain<ZB_M_WIN>(v, (const uint8_t ZB_LDSP*)nullptr, s.shift, og, nops, wc,
+#endif
                                   data, lane, &hl, &done, &hw);
     }
     ZB_STAMP(2);
