@@ -707,7 +707,7 @@ struct OpHeads {
     }
 };
 #ifndef ZB_OP_KINDS
-#define ZB_OP_KINDS 0          // run_chain's typestate pass reads the prefetched kinds
+#define ZB_OP_KINDS 1          // run_chain's typestate pass reads the prefetched kinds
 #endif
 
 __device__ __forceinline__ uint32_t sad4(uint4 q) {
