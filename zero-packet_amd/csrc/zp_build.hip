@@ -686,7 +686,9 @@ struct OpGlobal {
 #ifndef ZB_OP_PREFETCH
 #define ZB_OP_PREFETCH 1
 #endif
+#ifndef ZB_OPH
 #define ZB_OPH 4
+#endif
 struct OpHeads {
     OpGlobal og;
     uint2 h[ZB_OPH];
