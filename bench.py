@@ -24,8 +24,15 @@ Reported next to the GPU number:
                 from HIP events on the launch stream, vs 8.0 TB/s HBM peak
   cpu_baseline  the CPU oracle (a C port of the reference; the Rust original
                 cannot be built here) on a bounded sample of the same frames
+                (rank 0 at N = 1 only)
   h2d_d2h_inclusive  host-pinned frames -> H2D -> parse -> D2H (PCIe) rate on
-                a sample (zp_parse_batch_host); recorded, never `value`
+                a 2M-frame sample (zp_parse_batch_host), every rank at once,
+                frames summed over ranks / the slowest rank; never `value`
+  config5       BASELINE config 5 in the same ranks after the headline: the
+                256M-frame IMIX stream (--c5-frames) cut into N contiguous
+                shards (strong scaling), its own timed loop of --steps
+                launches, per-rank shards / rejected frames / roofline
+                fraction (--no-c5 skips it)
 """
 import argparse
 import importlib
@@ -58,6 +65,13 @@ C5_TOTAL = 1 << 28          # config 5: one 256M-frame stream over all ranks
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def parse_count(s):
+    """'8M' -> 8388608, '256M' -> 268435456, '4096' -> 4096 (K/M/G = 2^10/20/30)."""
+    s = str(s).strip()
+    mult = {"K": 1 << 10, "M": 1 << 20, "G": 1 << 30}.get(s[-1:].upper(), 1)
+    return int(s[:-1] if mult > 1 else s) * mult
 
 
 def host_cores():
@@ -157,8 +171,10 @@ def cpu_baseline(zp, arena, offs, lens, sample_pkts, min_seconds):
                       f"first {m1} frames, {reps1} passes"}
 
 
-def pcie_inclusive(zp, arena, offs, lens, sample_pkts):
-    """Host-pinned frames through zp_parse_batch_host (H2D + parse + D2H)."""
+def pcie_inclusive(zp, arena, offs, lens, sample_pkts, barrier=lambda: None):
+    """Host-pinned frames through zp_parse_batch_host (H2D + parse + D2H).
+    Every rank runs it at once between two barriers (each GPU has its own host
+    link); returns this rank's (frames, bytes, seconds per pass)."""
     m = min(sample_pkts, offs.numel())
     o = offs[:m].cpu().numpy().astype(np.uint64)
     ln = lens[:m].cpu().numpy().astype(np.uint32)
@@ -170,14 +186,79 @@ def pcie_inclusive(zp, arena, offs, lens, sample_pkts):
     ctx = lib.zp_ctx_create(torch.cuda.current_device(), 256 << 20)
     args = (ctx, host.data_ptr(), end, o.ctypes.data, ln.ctypes.data, m, recs.data_ptr(), None)
     zp._lib.check(lib.zp_parse_batch_host(*args), "zp_parse_batch_host")   # warm
+    barrier()
     reps, t0 = 3, time.perf_counter()
     for _ in range(reps):
         zp._lib.check(lib.zp_parse_batch_host(*args), "zp_parse_batch_host")
     sec = (time.perf_counter() - t0) / reps
+    barrier()
     lib.zp_ctx_destroy(ctx)
-    return {"mpkt_per_s": round(m / sec / 1e6, 2), "gb_per_s": round(end / sec / 1e9, 2),
-            "sample_frames": m, "path": "pinned host -> H2D -> kernel -> D2H records, "
-                                        "2 streams x 256 MiB chunks"}
+    errs = int((zp.batch.record_err(recs) != 0).sum().item())
+    assert errs == 0, f"host path: {errs} frames rejected"
+    return m, end, sec
+
+
+PCIE_PATH = "pinned host -> H2D -> kernel -> D2H records, 2 streams x 256 MiB chunks"
+
+
+def gather_rows(row, world, rank, dev):
+    """Every rank's float64 row as a [world, len(row)] numpy array (one
+    all-reduce of a zero-padded table; no data-path collective)."""
+    t = torch.zeros((world, len(row)), dtype=torch.float64, device=dev)
+    t[rank] = torch.tensor(row, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return t.cpu().numpy()
+
+
+def config5_leg(zp, total, steps, warmup, world, rank, dev, barrier, coll_dev):
+    """BASELINE config 5 in the same ranks: the `total`-frame IMIX stream cut
+    into `world` contiguous shards, rank r parsing frames [total*r/world,
+    total*(r+1)/world) (strong scaling: the job is fixed, N shares it). Timed
+    like the headline: barrier + synchronise around exactly `steps` launches,
+    max over ranks."""
+    first, end = total * rank // world, total * (rank + 1) // world
+    n = end - first
+    arena, offs, lens = zp.batch.generate("c5", n, first=first, device=dev)
+    records = torch.empty((n, zp.records.RECORD_BYTES), dtype=torch.uint8, device=dev)
+    ext = torch.empty((2, n, 16), dtype=torch.uint8, device=dev)
+    nbytes = int(lens.to(torch.int64).sum().item())
+    zp.batch.parse_batch(arena, offs, lens, records, ext, check=True)
+    torch.cuda.synchronize()
+    errs = int((zp.batch.record_err(records) != 0).sum().item())
+    for _ in range(warmup):
+        zp.batch.parse_batch(arena, offs, lens, records, ext, check=False)
+    stream = torch.cuda.current_stream(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(steps)]
+    torch.cuda.synchronize()
+    barrier()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        ev[k][0].record(stream)
+        zp.batch.parse_batch(arena, offs, lens, records, ext, check=False)
+        ev[k][1].record(stream)
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    kmean = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    del arena, offs, lens, records, ext
+    torch.cuda.empty_cache()
+    rows = gather_rows([first, end, nbytes, errs, kmean, elapsed], world, rank, coll_dev)
+    t = float(rows[:, 5].max())
+    job_bytes = int(rows[:, 2].sum())
+    return {
+        "workload": WORKLOADS["c5"].replace(" shard", "") + f", {total} frames split {world} ways",
+        "frames_total": total, "bytes_total": job_bytes, "scaling": "strong",
+        "steps": steps, "warmup": warmup, "ms_per_step": round(t / steps * 1e3, 4),
+        "mpkt_s": round(total * steps / t / 1e6, 2),
+        "gb_s": round(job_bytes * steps / t / 1e9, 2),
+        "shards": [[int(a), int(b)] for a, b in rows[:, 0:2]],
+        "rejected_per_rank": [int(x) for x in rows[:, 3]],
+        "kernel_ms_per_rank": [round(float(x), 4) for x in rows[:, 4]],
+        "frac_per_rank": [round(float(b) / (k * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                          for b, k in zip(rows[:, 2], rows[:, 4])],
+    }
 
 
 def main():
@@ -191,6 +272,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-pcie", action="store_true")
+    ap.add_argument("--c5-frames", type=str, default=str(C5_TOTAL),
+                    help="frames of the config-5 stream split over the ranks (e.g. 8M)")
+    ap.add_argument("--no-c5", action="store_true", help="skip the config-5 leg")
     args = ap.parse_args()
 
     if args.gpus < 1:
@@ -301,16 +385,33 @@ def main():
                      "kernel_ms_mean": round(kmean, 4), "kernel_ms_min": round(min(kms), 4),
                      "algorithmic_bytes_per_launch": total_bytes},
     }
-    if rank == 0 and world == 1:
-        if not args.no_pcie:
-            out["h2d_d2h_inclusive"] = pcie_inclusive(zp, arena, offs, lens, 1 << 21)
-        if not args.no_cpu:
-            out["cpu_baseline"] = cpu_baseline(zp, arena, offs, lens, args.cpu_sample,
-                                               args.cpu_seconds)
-            # vs_baseline stays null: BASELINE.md has no published number for
-            # this metric. The ratio to the CPU leg of this run is reported
-            # beside it instead.
-            out["vs_cpu_baseline"] = round(out["value"] / out["cpu_baseline"]["value"], 1)
+    coll_dev = "cpu" if shared else dev
+    if not args.no_pcie:
+        # every rank's host path at once: frames of all ranks / the slowest rank
+        m, nb, sec = pcie_inclusive(zp, arena, offs, lens, 1 << 21, barrier)
+        rows = gather_rows([m, nb, sec], world, rank, coll_dev)
+        t = float(rows[:, 2].max())
+        out["h2d_d2h_inclusive"] = {
+            "mpkt_per_s": round(float(rows[:, 0].sum()) / t / 1e6, 2),
+            "gb_per_s": round(float(rows[:, 1].sum()) / t / 1e9, 2),
+            "sample_frames": int(rows[:, 0].sum()), "ranks": world,
+            "per_rank_gb_per_s": [round(float(b) / s / 1e9, 2) for b, s in rows[:, 1:3]],
+            "path": PCIE_PATH + ("; all ranks concurrently, summed" if world > 1 else "")}
+    if rank == 0 and world == 1 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline(zp, arena, offs, lens, args.cpu_sample,
+                                           args.cpu_seconds)
+        # vs_baseline stays null: BASELINE.md has no published number for
+        # this metric. The ratio to the CPU leg of this run is reported
+        # beside it instead.
+        out["vs_cpu_baseline"] = round(out["value"] / out["cpu_baseline"]["value"], 1)
+    if args.config != "c5" and not args.no_c5:
+        # BASELINE config 5 (256M-frame IMIX over the N GPUs, strong scaling)
+        # in the same ranks, so every 1/2/4/8-GPU line carries it
+        del arena, offs, lens, records, ext
+        torch.cuda.empty_cache()
+        out["config5"] = config5_leg(zp, parse_count(args.c5_frames), args.steps, args.warmup,
+                                     world, rank, dev, barrier, coll_dev)
+        assert sum(out["config5"]["rejected_per_rank"]) == 0, "config 5: frames rejected"
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

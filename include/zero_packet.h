@@ -27,12 +27,15 @@
 extern "C" {
 #endif
 
-#define ZP_ABI_VERSION 4   /* 2: 16-B record, extension chains in the ext side array;
+#define ZP_ABI_VERSION 5   /* 2: 16-B record, extension chains in the ext side array;
                               3: reader-accessor error codes 36-37 (ZP_ERR_COUNT 38,
                                  ZP_STATS_COUNT 62), standalone readers and the
                                  checksum primitives (zp_reader_new, zp_*checksum*);
                               4: 8-B record (flags word + packed offsets); the IPv6
-                                 final next header of a chain in its ext entry */
+                                 final next header of a chain in its ext entry;
+                              5: the far-L4 form (Ethernet code 3, the whole L4
+                                 offset in `offs`) replaces v4's saturation at
+                                 ZP_L4_FAR; zp_rec_decode */
 
 /* ------------------------------------------------------------------------- */
 /* Per-packet parse error codes. One code per DISTINCT reference error string */
@@ -120,8 +123,8 @@ typedef enum zp_err {
  * 2-7 % off every configuration against the 16-B record of ABI v2/v3.
  *
  *   flags  bits  0-23  ZP_F_* presence and extension-slot bits (above)
- *          bits 24-25  Ethernet header length: 14 + 4 * code (14 / 18 / 22,
- *                      ethernet.rs:155-179)
+ *          bits 24-25  Ethernet code: header length 14 + 4 * code (14 / 18 /
+ *                      22, ethernet.rs:155-179); code 3 = the far-L4 form
  *          bits 26-31  err (zp_err; ZP_OK = 0)
  *   offs   bits  0-17  l4_off: start of the single tcp/udp/icmpv4/icmpv6 reader
  *          bits 18-31  inner_off: start of the ip_in_ip header (always below
@@ -129,11 +132,20 @@ typedef enum zp_err {
  *
  * All offsets are FRAME offsets (bytes from the first byte of the frame).
  * ethernet/arp/ipv4/ipv6 start at offsets 0 / eth_len / eth_len / eth_len.
- * An L4 header that starts at byte ZP_L4_FAR (262,143) or later, which only
- * an IPv6 jumbogram with dozens of nested maximal headers reaches, is
- * reported as ZP_L4_FAR; the facades refuse such a record.
  * When err != ZP_OK the reference returns Err and no PacketParser exists:
  * the record is then zero except the err bits.
+ *
+ * Far-L4 form (ABI v5). An L4 reader that starts past ZP_L4_NEAR_MAX
+ * (262,143) does not fit 18 bits; only an IPv6 jumbogram with thousands of
+ * nested IPv6 headers reaches it (parser.rs:134-135 recurses without limit,
+ * ipv6.rs:147-167 never checks payload_length). Its record carries Ethernet
+ * code 3 and offs = the whole 32-bit L4 offset. The Ethernet header length
+ * and inner_off, which such a frame always has (its first IP level ends by
+ * byte 9,290), are then read from the frame, exactly as the parse found them:
+ * eth_len by ethernet.rs:155-179, inner_off = eth_len + the outer IP header
+ * (IPv4: IHL * 4; IPv6: 40 + extension_headers_len, the outer ext entry's
+ * len). zp_rec_decode() does this; the facades call it. Every result stays
+ * exact: nothing saturates.
  *
  * IPv6Reader::final_next_header() (ipv6.rs:219-227) is not in the record:
  * for an IPv6 header with an extension chain it is the chain's
@@ -145,12 +157,15 @@ typedef struct zp_record {
     uint32_t offs;
 } zp_record;
 
-#define ZP_F_MASK   0x00FFFFFFu
-#define ZP_L4_FAR   0x3FFFFu
-static inline uint32_t zp_rec_err(zp_record r)       { return r.flags >> 26; }
-static inline uint32_t zp_rec_eth_len(zp_record r)   { return 14u + 4u * ((r.flags >> 24) & 3u); }
-static inline uint32_t zp_rec_l4_off(zp_record r)    { return r.offs & ZP_L4_FAR; }
-static inline uint32_t zp_rec_inner_off(zp_record r) { return r.offs >> 18; }
+#define ZP_F_MASK        0x00FFFFFFu
+#define ZP_L4_NEAR_MAX   0x3FFFFu   /* largest l4_off of the ordinary form   */
+#define ZP_ETH_CODE_FAR  3u         /* flags bits 24-25 of the far-L4 form   */
+static inline uint32_t zp_rec_err(zp_record r)     { return r.flags >> 26; }
+static inline int      zp_rec_is_far(zp_record r)  { return ((r.flags >> 24) & 3u) == ZP_ETH_CODE_FAR; }
+static inline uint32_t zp_rec_l4_off(zp_record r)  { return zp_rec_is_far(r) ? r.offs : r.offs & ZP_L4_NEAR_MAX; }
+/* Ordinary form only (0 for a far-L4 record: zp_rec_decode reads them from the frame). */
+static inline uint32_t zp_rec_eth_len(zp_record r)   { return zp_rec_is_far(r) ? 0u : 14u + 4u * ((r.flags >> 24) & 3u); }
+static inline uint32_t zp_rec_inner_off(zp_record r) { return zp_rec_is_far(r) ? 0u : r.offs >> 18; }
 
 /*
  * One IPv6 extension chain (Some(ExtensionHeaders), headers.rs:19-28), 16 B:
@@ -171,6 +186,26 @@ typedef struct zp_ext_offsets {
     uint8_t  final_nh;
     uint8_t  reserved;
 } zp_ext_offsets;
+
+/* A record with every field unpacked (PacketParser's readers by start
+ * offset): flags = ZP_F_* bits, eth_len 14/18/22, final_nh / inner_final_nh
+ * = IPv6Reader::final_next_header() (ipv6.rs:219-227) of the outer /
+ * ip_in_ip IPv6 header (0 where absent); all zero but err on an error. */
+typedef struct zp_rec_fields {
+    uint32_t flags;
+    uint8_t  err, eth_len, final_nh, inner_final_nh;
+    uint32_t inner_off, l4_off;
+} zp_rec_fields;
+
+/* Unpacks `*rec`, the record of `frame` (len bytes), both forms (see above).
+ * ext: NULL or the frame's two entries (outer chain, ip_in_ip chain); where
+ * the record flags a chain and ext is NULL the chain is re-walked over the
+ * frame (ipv6.rs:147-167), which gives the same values for a frame the
+ * parse accepted. Host code. Returns 0, or -1 when the record cannot belong
+ * to this frame (an offset past its end, a far record without an L4 reader
+ * or an ip_in_ip header). */
+int zp_rec_decode(const zp_record* rec, const uint8_t* frame, uint64_t len,
+                  const zp_ext_offsets* ext, zp_rec_fields* out);
 
 /* ------------------------------------------------------------------------- */
 /* Library info                                                              */

@@ -448,7 +448,19 @@ struct PacketParser {
         if (((flags & ZP_F_EXT) && !outer) || ((flags & ZP_F_INNER_EXT) && !inner))
             throw std::invalid_argument("from_record: the record flags an extension chain");
         PacketParser p;
-        const size_t hl = zp_rec_eth_len(r), io = zp_rec_inner_off(r);
+        // both record forms: the far-L4 one (ABI v5) reads the Ethernet header
+        // length and the ip_in_ip offset from the frame (zp_rec_decode)
+        size_t hl = zp_rec_eth_len(r), io = zp_rec_inner_off(r);
+        if (zp_rec_is_far(r)) {
+            // (zp_rec_decode restated, header-only) ethernet.rs:155-179, then
+            // the ip_in_ip header behind the outer IP header
+            if (!(flags & ZP_F_IP_IN_IP) || frame.len < 62)
+                throw std::invalid_argument("from_record: far-L4 record without ip_in_ip");
+            const uint32_t t = detail::be16(frame, 12);
+            hl = t == 0x8100 ? 18 : t == 0x88A8 ? 22 : 14;
+            io = (flags & ZP_F_IPV6) ? hl + 40 + ((flags & ZP_F_EXT) ? outer->len : 0)
+                                     : hl + (frame[hl] & 15u) * 4;   // ipv4.rs:228-258
+        }
         if (flags & ZP_F_ETHERNET) p.ethernet.emplace(frame, hl);
         if (flags & ZP_F_ARP) p.arp.emplace(frame.sub(hl));
         if (flags & ZP_F_IPV4) p.ipv4.emplace(frame.sub(hl));
@@ -479,11 +491,7 @@ struct PacketParser {
             }
             p.ip_in_ip = ii;
         }
-        const uint32_t l4_off = zp_rec_l4_off(r);
-        constexpr uint32_t l4_any = ZP_F_TCP | ZP_F_UDP | ZP_F_ICMPV4 | ZP_F_ICMPV6;
-        if ((flags & l4_any) && l4_off == ZP_L4_FAR)
-            throw std::invalid_argument("from_record: L4 header past ZP_L4_FAR (not in the record)");
-        const Bytes l4 = frame.sub(l4_off);
+        const Bytes l4 = frame.sub(zp_rec_l4_off(r));
         if (flags & ZP_F_TCP) p.tcp.emplace(l4);
         if (flags & ZP_F_UDP) p.udp.emplace(l4);
         if (flags & ZP_F_ICMPV4) p.icmpv4.emplace(l4);

@@ -365,7 +365,8 @@ typedef struct zpo_record {
 } zpo_record;
 
 /* zp_record (include/zero_packet.h): flags | Ethernet code << 24 | err << 26,
- * l4_off (saturated at ZP_L4_FAR) | inner_off << 18. */
+ * l4_off | inner_off << 18; an l4_off past ZP_L4_NEAR_MAX in the far-L4 form
+ * (code 3, offs = l4_off; ABI v5). */
 void zpo_pack(const zpo_record* full, uint64_t n, zp_record* out) {
     for (uint64_t i = 0; i < n; ++i) {
         const zpo_record* r = &full[i];
@@ -374,8 +375,13 @@ void zpo_pack(const zpo_record* full, uint64_t n, zp_record* out) {
             out[i].offs = 0;
             continue;
         }
+        if (r->l4_off > ZP_L4_NEAR_MAX) {
+            out[i].flags = r->flags | ZP_ETH_CODE_FAR << 24;
+            out[i].offs = r->l4_off;
+            continue;
+        }
         out[i].flags = r->flags | ((uint32_t)(r->eth_len - 14) / 4u) << 24;
-        out[i].offs = (r->l4_off < ZP_L4_FAR ? r->l4_off : ZP_L4_FAR) | r->inner_off << 18;
+        out[i].offs = r->l4_off | r->inner_off << 18;
     }
 }
 

@@ -52,7 +52,7 @@ def test_err_strings(zp):
         35: "IPv6 encapsulated checksum is invalid.",
     }
     lib = zp._lib.hip()
-    assert lib.zp_abi_version() == 4
+    assert lib.zp_abi_version() == 5
     assert lib.zp_err_str(0) == b""
     for code, s in want.items():
         assert lib.zp_err_str(code).decode() == s
@@ -62,7 +62,7 @@ def test_err_strings(zp):
 
 
 def test_record_layout(zp):
-    """zp_record / zp_ext_offsets (ABI v4) as the numpy dtypes see them, and
+    """zp_record / zp_ext_offsets (ABI v5) as the numpy dtypes see them, and
     unpack() decoding the packed fields."""
     r, e = zp.records.RECORD_DTYPE, zp.records.EXT_DTYPE
     assert r.itemsize == 8 and e.itemsize == 16
@@ -71,10 +71,12 @@ def test_record_layout(zp):
     rec = np.zeros(3, r)
     rec[0] = (zp.records.F_ETHERNET | zp.records.F_IPV6 | zp.records.F_TCP | 2 << 24, 170 | 150 << 18)
     rec[1] = (29 << 26, 0)                                   # Err(UDP_LENGTH)
-    rec[2] = (zp.records.F_ETHERNET | 1 << 24, zp.records.L4_FAR)
+    rec[2] = (zp.records.F_ETHERNET | zp.records.F_IPV6 | zp.records.F_IP_IN_IP |
+              zp.records.F_UDP | 3 << 24, 264014)              # far-L4 form (ABI v5)
     u = zp.records.unpack(rec)
-    assert list(u["err"]) == [0, 29, 0] and list(u["eth_len"]) == [22, 0, 18]
-    assert list(u["l4_off"]) == [170, 0, zp.records.L4_FAR] and list(u["inner_off"]) == [150, 0, 0]
+    assert list(u["err"]) == [0, 29, 0] and list(u["eth_len"]) == [22, 0, 0]
+    assert list(u["l4_off"]) == [170, 0, 264014] and list(u["inner_off"]) == [150, 0, 0]
+    assert list(zp.records.is_far(rec)) == [False, False, True]
     assert u["flags"][0] == zp.records.F_ETHERNET | zp.records.F_IPV6 | zp.records.F_TCP
     assert list(zp.records.rec_err(rec)) == [0, 29, 0]
 

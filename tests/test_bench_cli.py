@@ -25,3 +25,13 @@ def test_host_cores_reports_affinity():
     assert 1 <= threads <= visible
     if quota is not None:
         assert threads <= max(1, int(quota))
+
+
+def test_parse_count_suffixes():
+    sys.path.insert(0, ROOT)
+    import bench
+    assert bench.parse_count("8M") == 8 << 20
+    assert bench.parse_count("256m") == 1 << 28
+    assert bench.parse_count("4096") == 4096
+    assert bench.parse_count("2K") == 2048
+    assert bench.parse_count(str(bench.C5_TOTAL)) == bench.C5_TOTAL

@@ -15,6 +15,8 @@ packet. The hand-written strings below are kept as readable examples.
 """
 import re
 
+import pytest
+
 import oracle as orc
 from test_getters import READER_CLS, built
 
@@ -180,3 +182,45 @@ def test_debug_follows_the_reference_impls(zp, golden):
         assert p.debug() == _expect(zp, p, D), fx["name"]
         n += 1
     assert n >= 8 and seen == set(READER_CLS.values())
+
+
+@pytest.mark.gpu
+def test_debug_of_gpu_records(zp, golden):
+    """Row f4 through the product path: the golden packets, 2,048 c5 frames,
+    512 c4 frames (extension chains) and the far-L4 frames parsed ON THE GPU,
+    through the device batch (zp_parse_batch_device) and through
+    PacketParser.parse (zp_parse_one). Their {:?} and {:#?} text equals the
+    text of the oracle's records and the text the reference's Debug impls
+    give (misc.rs:243-290, ipv4.rs:267-287, ...)."""
+    import numpy as np
+    import torch
+    from test_l4_far import CASES, deep_frame
+    D = golden["debug_impls"]
+    frames = [bytes.fromhex(fx["bytes"]) for fx in golden["fixtures"]]
+    for cfg, n in (("c5", 2048), ("c4", 512)):
+        a, o, l = zp.batch.generate_host(cfg, n, first=777)
+        frames += [a[int(o[i]):int(o[i]) + int(l[i])].tobytes() for i in range(n)]
+    frames += [deep_frame(lv, **kw)[0] for lv, kw in CASES]
+    offs = np.cumsum([0] + [len(f) for f in frames[:-1]]).astype(np.int64)
+    arena = np.frombuffer(b"".join(frames) + bytes(64), np.uint8).copy()
+    lens = np.array([len(f) for f in frames], np.int32)
+    d = torch.device("cuda:0")
+    r, e = zp.batch.parse_batch(torch.from_numpy(arena).to(d), torch.from_numpy(offs).to(d),
+                                torch.from_numpy(lens).to(d))
+    got, gext = zp.batch.records_to_numpy(r, e)
+    ok = 0
+    for k, f in enumerate(frames):
+        err, rec, ext = orc.parse_one_abi(f)
+        assert int(got[k]["flags"]) >> 26 == err
+        if err:
+            continue
+        want = zp.PacketParser.from_record(f, rec, ext)
+        batch = zp.PacketParser.from_record(f, got[k], gext[:, k])
+        one = zp.PacketParser.parse(f)
+        text = want.debug()
+        assert text == _expect(zp, want, D)
+        assert batch.debug() == text and one.debug() == text, k
+        pretty = want.debug(pretty=True)
+        assert batch.debug(pretty=True) == pretty and one.debug(pretty=True) == pretty, k
+        ok += 1
+    assert ok >= 2560

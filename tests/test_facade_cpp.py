@@ -103,6 +103,9 @@ def _frames(zp, golden):
             if i % 3 == 0:
                 f[int(rng.integers(0, len(f)))] ^= int(rng.integers(1, 256))
                 frames.append(bytes(f))
+    # L4 readers past byte 262,143: the record's far-L4 form (ABI v5)
+    from test_l4_far import CASES, deep_frame
+    frames += [deep_frame(lv, **kw)[0] for lv, kw in CASES]
     return frames
 
 
@@ -127,6 +130,7 @@ def test_cpp_facade_from_record_matches_python_facade(zp, golden):
     assert sum(1 for _, r, _, _ in exp if int(r["flags"]) >> 26) > 10
     assert any("iip6:" in s for *_, s in exp) and any(";ext=-" not in s and "ipv6" in s
                                                       for *_, s in exp)
+    assert sum(1 for _, r, _, _ in exp if (int(r["flags"]) >> 24) & 3 == 3) == 4   # far-L4
 
 
 @pytest.mark.gpu

@@ -271,3 +271,32 @@ def test_checksum_primitives(zp, golden, built):
     assert out == want
     with pytest.raises(ValueError):
         zp.pseudo_header(bytes(4), bytes(16), 6, 20)
+
+
+def test_host_helpers_without_the_library(zp, golden, monkeypatch):
+    """internet_checksum and the EthernetReader view keep working when
+    libzp_hip.so cannot be loaded: the Python restatements give
+    the checksum.rs:75-133 answers and the oracle's values."""
+    import importlib
+    parser = importlib.import_module("zero-packet_amd.parser")
+    monkeypatch.setattr(parser, "_lib_available", lambda: False)
+    for kat in golden["checksum_kats"]:
+        d = bytes(kat["data"])
+        assert parser.internet_checksum(d, kat["acc"]) == kat["checksum"], kat["source"]
+    rng = random.Random(9)
+    for _ in range(200):
+        d = bytes(rng.randrange(256) for _ in range(rng.randrange(1, 200)))
+        acc = rng.choice([0, rng.randrange(1 << 32), 0xFFFFFFFF - rng.randrange(64)])
+        assert parser.internet_checksum(d, acc) == orc.internet_checksum(d, acc)
+    big = b"\xff" * (1 << 17) + b"\x01\x02\x03"
+    assert parser.internet_checksum(big, 0xFFFF0000) == orc.internet_checksum(big, 0xFFFF0000)
+    for fx in golden["fixtures"]:
+        f = bytes.fromhex(fx["bytes"])
+        want = orc.reader_new(0, f)
+        if want[0] == 0:
+            assert parser.EthernetReader(f).header_len() == want[1]
+        else:
+            with pytest.raises(parser.ZeroPacketError):
+                parser.EthernetReader(f)
+    with pytest.raises(parser.ZeroPacketError):
+        parser.EthernetReader(bytes(13))

@@ -103,7 +103,7 @@ def main():
     print(f"zp_parse_batch_host (2 x 256 MiB): {total / dt / 1e9:6.2f} GB/s "
           f"{len(offs) / dt / 1e6:7.1f} Mpkt/s", flush=True)
     lib.zp_ctx_destroy(ctx)
-    assert (out["err"] == 0).all()
+    assert (zp.records.rec_err(out) == 0).all()
 
 
 if __name__ == "__main__":

@@ -54,6 +54,7 @@ def hip():
         _sig(lib, "zp_internet_checksum", ctypes.c_uint16, [vp, u64, u32])
         _sig(lib, "zp_verify_internet_checksum", i32, [vp, u64, u32])
         _sig(lib, "zp_pseudo_header", u32, [vp, vp, u32, ctypes.c_uint8, u64])
+        _sig(lib, "zp_rec_decode", i32, [vp, vp, u64, vp, vp])
         _hip = lib
     return _hip
 

@@ -25,10 +25,13 @@ struct zp_rec_full {
     uint32_t inner_off, l4_off;
 };
 
+// The 8-B record (include/zero_packet.h); an L4 reader past ZP_L4_NEAR_MAX
+// takes the far-L4 form: Ethernet code 3, the whole offset in `offs`.
 __device__ __forceinline__ zp_u32x2 zp_pack(const zp_rec_full& r) {
     if (r.err) return zp_u32x2{(uint32_t)r.err << 26, 0u};
-    const uint32_t l4 = r.l4_off < ZP_L4_FAR ? r.l4_off : ZP_L4_FAR;
-    return zp_u32x2{r.flags | ((uint32_t)(r.eth_len - 14) >> 2) << 24, l4 | (r.inner_off << 18)};
+    const bool far = r.l4_off > ZP_L4_NEAR_MAX;
+    const uint32_t code = far ? ZP_ETH_CODE_FAR : (uint32_t)(r.eth_len - 14) >> 2;
+    return zp_u32x2{r.flags | code << 24, far ? r.l4_off : r.l4_off | (r.inner_off << 18)};
 }
 
 // A reader R gives frame byte x as rd(x), and bytes [x, x + 4) as one

@@ -53,6 +53,7 @@ struct zp_ctx {
     // ext entries, frame) the kernel reads and writes in place
     uint8_t* one_h;
     uint8_t* one_d;
+    bool one_failed;              // the mapped block could not be allocated: batch path
 };
 
 // zp_parse_one's block: the frame at ONE_FRAME, its descriptor in front, the
@@ -280,7 +281,7 @@ extern "C" int zp_parse_one(zp_ctx* c, const uint8_t* frame, uint64_t len,
     int prev = 0;
     (void)hipGetDevice(&prev);
     if (hipSetDevice(c->device) != hipSuccess) return -2;
-    if (!c->one_h && len <= ONE_MAX) {
+    if (!c->one_h && !c->one_failed && len <= ONE_MAX) {
         hipError_t a = hipHostMalloc((void**)&c->one_h, ONE_FRAME + ONE_MAX + 64,
                                      hipHostMallocMapped | hipHostMallocCoherent);
         if (a == hipSuccess) a = hipHostGetDevicePointer((void**)&c->one_d, c->one_h, 0);
@@ -288,6 +289,7 @@ extern "C" int zp_parse_one(zp_ctx* c, const uint8_t* frame, uint64_t len,
             (void)hipGetLastError();
             (void)hipHostFree(c->one_h);
             c->one_h = c->one_d = NULL;
+            c->one_failed = true;                   // not retried on every call
         }
     }
     if (len > ONE_MAX || !c->one_h) {

@@ -86,8 +86,9 @@ struct HdrReader {
 // `ip`: its next-header byte, or with an extension chain the next-header
 // byte of the chain's last header (headers.rs:51-213 stops after the
 // headers the slot bits name; lengths by type as in the walk).
+// *end = the upper-layer payload's start (ipv6.rs:283-285).
 template <class R>
-__device__ __forceinline__ uint32_t final_nh(R& rd, uint32_t ip, uint32_t slots) {
+__device__ __forceinline__ uint32_t final_nh(R& rd, uint32_t ip, uint32_t slots, uint32_t* end) {
     uint32_t cur = rd(ip + 6), p = ip + 40;
     for (int k = __builtin_popcount(slots & 63u); k > 0; --k) {
         const uint32_t b1 = rd(p + 1);
@@ -95,6 +96,7 @@ __device__ __forceinline__ uint32_t final_nh(R& rd, uint32_t ip, uint32_t slots)
         cur = rd(p);
         p += hl;
     }
+    *end = p;
     return cur;
 }
 
@@ -111,19 +113,19 @@ zp_columns_kernel(const uint8_t* __restrict__ arena, const uint64_t* __restrict_
     // the 8-B record, unpacked (include/zero_packet.h); the final next
     // headers of the IPv6 readers come from the frame after the staging
     zp_rec_full r;
-    {
-        static_assert(sizeof(zp_record) == 8, "one 8-B load per record");
-        const zp_u32x2 q = *(const FX_GLOBAL zp_u32x2*)(recs + i);
-        r.flags = q.x & ZP_F_MASK;
-        r.err = (uint8_t)(q.x >> 26);
-        r.eth_len = (uint8_t)(14u + 4u * ((q.x >> 24) & 3u));
-        r.final_nh = 0;
-        r.inner_final_nh = 0;
-        r.l4_off = q.y & ZP_L4_FAR;
-        r.inner_off = q.y >> 18;
-        // an L4 header past ZP_L4_FAR is not in the record: no L4 columns
-        if (r.l4_off == ZP_L4_FAR) r.flags &= ~(uint32_t)(ZP_F_TCP | ZP_F_UDP | ZP_F_ICMPV4 | ZP_F_ICMPV6);
-    }
+    static_assert(sizeof(zp_record) == 8, "one 8-B load per record");
+    const zp_u32x2 q = *(const FX_GLOBAL zp_u32x2*)(recs + i);
+    r.flags = q.x & ZP_F_MASK;
+    r.err = (uint8_t)(q.x >> 26);
+    r.final_nh = 0;
+    r.inner_final_nh = 0;
+    // The far-L4 form (an L4 reader past byte 262,143): offs holds the whole
+    // L4 offset; the Ethernet header length and inner_off are read from the
+    // frame after the staging (include/zero_packet.h).
+    const bool far = ((q.x >> 24) & 3u) == ZP_ETH_CODE_FAR;
+    r.eth_len = (uint8_t)(far ? 22u : 14u + 4u * ((q.x >> 24) & 3u));
+    r.l4_off = far ? q.y : q.y & ZP_L4_NEAR_MAX;
+    r.inner_off = far ? 0u : q.y >> 18;
     const bool ok = live && r.err == 0 && (r.flags & ZP_F_ETHERNET);
     const uint32_t len = ok ? lens[i] : 0u;
     const uintptr_t ga = (uintptr_t)arena + (ok ? offs[i] : 0);
@@ -140,6 +142,7 @@ zp_columns_kernel(const uint8_t* __restrict__ arena, const uint64_t* __restrict_
         if (r.flags & (ZP_F_TCP | ZP_F_UDP | ZP_F_ICMPV4 | ZP_F_ICMPV6))
             need = r.l4_off + 20 > need ? r.l4_off + 20 : need;
     }
+    if (far) need = FX_WIN;             // eth_len / inner_off not known yet
     need = need < len ? need : len;
     h.wlen = need < FX_WIN - h.shift ? need : FX_WIN - h.shift;
     h.win = (const uint8_t*)&win[threadIdx.x];
@@ -176,9 +179,17 @@ zp_columns_kernel(const uint8_t* __restrict__ arena, const uint64_t* __restrict_
 
     if (!live) return;
     HdrReader rd{h};
-    if (ok && (r.flags & ZP_F_IPV6)) r.final_nh = (uint8_t)final_nh(rd, r.eth_len, r.flags >> 12);
+    if (ok && far) {
+        const uint32_t t0 = rd16(rd, 12u);                          // ethernet.rs:155-179
+        r.eth_len = (uint8_t)(t0 == 0x8100 ? 18u : t0 == 0x88A8 ? 22u : 14u);
+    }
+    uint32_t ulp = 0;
+    if (ok && (r.flags & ZP_F_IPV6))
+        r.final_nh = (uint8_t)final_nh(rd, r.eth_len, r.flags >> 12, &ulp);
+    if (ok && far)                      // ip_in_ip follows the outer IP header
+        r.inner_off = (r.flags & ZP_F_IPV6) ? ulp : r.eth_len + (rd(r.eth_len) & 15u) * 4u;
     if (ok && (r.flags & ZP_F_IP_IN_IP_V6))
-        r.inner_final_nh = (uint8_t)final_nh(rd, r.inner_off, r.flags >> 18);
+        r.inner_final_nh = (uint8_t)final_nh(rd, r.inner_off, r.flags >> 18, &ulp);
     emit_columns(rd, r, ok, len, i, c);
 }
 

@@ -661,13 +661,19 @@ __device__ __forceinline__ bool fast_v4(const FrameView& f, Walk& w) {
 // Like fast_v4 it accepts a frame only when walk_frame would accept it with
 // exactly these readers and this record; any other frame (other stacks, any
 // failing check) is left to walk_frame, which finds the reference's first
-// error. Every header field it reads lies in the window (offsets < 72 and
-// frames >= 64 B: wlen >= 64; garbage past a short frame is never accepted,
-// its length checks fail first), except the L4 word and the pseudo-header
-// addresses of a deep stack, which take the window-or-global readers.
+// error. Every header field it reads lies in the window, except the L4 word
+// and the pseudo-header addresses of a deep stack, which take the
+// window-or-global readers. The highest byte read from the window is 81: the
+// encapsulated IPv4 header sum (wsum4<5>, bytes [62, 82)) behind Q-in-Q (22)
+// + IPv6 (40). The window holds min(len, ZP_WIN - 15) bytes of a frame, so
+// every frame of >= 82 bytes has them there; a shorter one fails that
+// level's `pos + 20 <= len` check whatever the bytes past it hold.
 // --------------------------------------------------------------------------
 #ifndef ZP_FAST_IP
 #define ZP_FAST_IP 1
+#endif
+#if ZP_FAST_IP
+static_assert(ZP_WIN - 15 >= 82, "fast_ip reads frame bytes up to 81 from the window");
 #endif
 struct IpLevel { uint32_t proto, next; bool ok; };
 // One IP level at `pos` (parser.rs:188-212 with a 20-B header / 222-230

@@ -7,6 +7,7 @@
  *   zp_internet_checksum        internet_checksum          (checksum.rs:5-29)
  *   zp_verify_internet_checksum verify_internet_checksum   (checksum.rs:33-35)
  *   zp_pseudo_header            pseudo_header              (checksum.rs:38-69)
+ *   zp_rec_decode               a zp_record unpacked (both forms, include/zero_packet.h)
  *
  * These are host functions over one host slice, as in the reference: a
  * reader is a view, its constructor checks a minimum length (Ethernet also
@@ -153,4 +154,77 @@ int zp_reader_new(int kind, const uint8_t* bytes, uint64_t len, zp_reader_info* 
     case ZP_READER_ICMPV6:   return len < 8 ? ZP_ERR_ICMP_TOO_SHORT : ZP_OK;          /* icmpv6.rs:90 */
     }
     return -1;
+}
+
+/* IPv6 header at frame[ip..]: its extension chain's length and
+ * final_next_header (ipv6.rs:141, :219-227), from the caller's entry when it
+ * has one, else by the walk IPv6Reader::new runs (ipv6.rs:159). */
+static int ipv6_chain(const uint8_t* frame, uint64_t len, uint64_t ip, int chained,
+                      const zp_ext_offsets* x, uint32_t* chain_len, uint8_t* final_nh) {
+    if (ip + 40 > len) return -1;
+    if (!chained) {
+        *chain_len = 0;
+        *final_nh = frame[ip + 6];
+        return 0;
+    }
+    if (x) {
+        *chain_len = x->len;
+        *final_nh = x->final_nh;
+        return 0;
+    }
+    zp_reader_info info;
+    if (zp_reader_new(ZP_READER_IPV6, frame + ip, len - ip, &info) != ZP_OK ||
+        !(info.flags & ZP_F_EXT))
+        return -1;
+    *chain_len = info.ext.len;
+    *final_nh = info.final_nh;
+    return 0;
+}
+
+int zp_rec_decode(const zp_record* rec, const uint8_t* frame, uint64_t len,
+                  const zp_ext_offsets* ext, zp_rec_fields* out) {
+    if (!rec || !out || (!frame && len)) return -1;
+    memset(out, 0, sizeof *out);
+    const zp_record r = *rec;
+    out->err = (uint8_t)zp_rec_err(r);
+    if (out->err) return 0;                         /* Err: no readers */
+    const uint32_t flags = r.flags & ZP_F_MASK;
+    out->flags = flags;
+    out->l4_off = zp_rec_l4_off(r);
+    const uint32_t l4_any = ZP_F_TCP | ZP_F_UDP | ZP_F_ICMPV4 | ZP_F_ICMPV6;
+    uint32_t outer_chain = 0;
+    if (zp_rec_is_far(r)) {
+        zp_reader_info eth;
+        if (!(flags & l4_any) || !(flags & ZP_F_IP_IN_IP) ||
+            zp_reader_new(ZP_READER_ETHERNET, frame, len, &eth) != ZP_OK)
+            return -1;
+        out->eth_len = (uint8_t)eth.header_len;                  /* ethernet.rs:155-179 */
+    } else {
+        out->eth_len = (uint8_t)zp_rec_eth_len(r);
+        out->inner_off = zp_rec_inner_off(r);
+    }
+    const uint64_t hl = out->eth_len;
+    if (flags & ZP_F_IPV6) {
+        if (ipv6_chain(frame, len, hl, (flags & ZP_F_EXT) != 0, ext ? &ext[0] : NULL,
+                       &outer_chain, &out->final_nh))
+            return -1;
+    }
+    if (zp_rec_is_far(r)) {
+        /* the ip_in_ip header follows the outer IP header (parser.rs:134-135) */
+        if (flags & ZP_F_IPV4) {
+            if (hl >= len) return -1;
+            out->inner_off = (uint32_t)hl + (frame[hl] & 15u) * 4u;   /* ipv4.rs:228-258 */
+        } else if (flags & ZP_F_IPV6) {
+            out->inner_off = (uint32_t)hl + 40u + outer_chain;         /* ipv6.rs:283-285 */
+        } else {
+            return -1;
+        }
+    }
+    if ((flags & ZP_F_IP_IN_IP_V6) &&
+        ipv6_chain(frame, len, out->inner_off, (flags & ZP_F_INNER_EXT) != 0,
+                   ext ? &ext[1] : NULL, &outer_chain, &out->inner_final_nh))
+        return -1;
+    if ((flags & ZP_F_IP_IN_IP) && out->inner_off >= len) return -1;
+    if ((flags & l4_any) && out->l4_off >= len) return -1;
+    return 0;
 }

@@ -52,16 +52,32 @@ def _buf(data):
     return data, ctypes.create_string_buffer(data, max(len(data), 1))
 
 
+def _py_internet_checksum(data, accumulator):
+    """checksum.rs:5-29 in Python (used when libzp_hip.so cannot be loaded):
+    big-endian words, an odd tail byte as the high byte, u32 wrap-around,
+    fold, complement."""
+    n = len(data) & ~1
+    words = np.frombuffer(data[:n], dtype=">u2").astype(np.uint64)
+    s = int(words.sum()) + accumulator + ((data[-1] << 8) if len(data) & 1 else 0)
+    s &= 0xFFFFFFFF
+    while s >> 16:
+        s = (s & 0xFFFF) + (s >> 16)
+    return ~s & 0xFFFF
+
+
 def internet_checksum(data, accumulator=0):
-    """internet_checksum (checksum.rs:5-29) via zp_internet_checksum."""
+    """internet_checksum (checksum.rs:5-29) via zp_internet_checksum; the
+    Python restatement when the library is not loadable (host helper, not
+    the parse path)."""
     data, b = _buf(data)
+    if not _lib_available():
+        return _py_internet_checksum(data, accumulator & 0xFFFFFFFF)
     return int(_lib.hip().zp_internet_checksum(b, len(data), accumulator & 0xFFFFFFFF))
 
 
 def verify_internet_checksum(data, accumulator=0):
     """verify_internet_checksum (checksum.rs:33-35)."""
-    data, b = _buf(data)
-    return bool(_lib.hip().zp_verify_internet_checksum(b, len(data), accumulator & 0xFFFFFFFF))
+    return internet_checksum(data, accumulator) == 0
 
 
 def pseudo_header(src, dest, protocol, length):
@@ -112,7 +128,12 @@ class EthernetReader(_Reader):
     def __init__(self, data, header_len=None):
         super().__init__(data)
         if header_len is None:
-            header_len = int(_reader_new(self.KIND, self.bytes)[1]["header_len"])
+            if _lib_available():
+                header_len = int(_reader_new(self.KIND, self.bytes)[1]["header_len"])
+            else:                               # ethernet.rs:141-179 without the library
+                if len(self.bytes) < 14:
+                    raise ZeroPacketError("Slice is too short to contain an Ethernet frame.", 2)
+                header_len = self.calculate_header_len(self.bytes)
         self._hl = header_len
 
     @classmethod
@@ -481,7 +502,7 @@ class PacketParser:
         ip_in_ip chain; EXT_DTYPE [2]), needed when the record flags a chain.
         Raises ZeroPacketError when the record holds an error."""
         frame = bytes(frame)
-        word, offs = int(rec["flags"]), int(rec["offs"])
+        word = int(rec["flags"])
         err = word >> 26
         if err:
             raise ZeroPacketError(_lib.hip().zp_err_str(err).decode() if _lib_available()
@@ -489,8 +510,10 @@ class PacketParser:
         flags = word & _rec.F_MASK
         if flags & (F_EXT | F_INNER_EXT) and ext is None:
             raise ValueError("the record flags an IPv6 extension chain: pass its ext entries")
+        # both record forms (the far-L4 one reads eth_len / inner_off from the frame)
+        d = _rec.decode(frame, rec, ext)
         p = cls()
-        hl = 14 + 4 * ((word >> 24) & 3)
+        hl, io, l4 = d["eth_len"], d["inner_off"], d["l4_off"]
         if flags & F_ETHERNET:
             p.ethernet = EthernetReader(frame, hl)
         if flags & F_ARP:
@@ -504,7 +527,6 @@ class PacketParser:
                 eh = _ext_from(frame, hl + 40, flags, 12, x["off"], x["len"], x["final_nh"])
             p.ipv6 = IPv6Reader(frame[hl:], eh, int(ext[0]["len"]) if eh else 0)
         if flags & F_IP_IN_IP:
-            io = offs >> 18
             if flags & F_IP_IN_IP_V6:
                 eh = None
                 if flags & F_INNER_EXT:
@@ -514,10 +536,6 @@ class PacketParser:
                                                        int(ext[1]["len"]) if eh else 0))
             else:
                 p.ip_in_ip = IpInIp("ipv4", IPv4Reader(frame[io:]))
-        l4 = offs & _rec.L4_FAR
-        if l4 == _rec.L4_FAR and flags & (F_TCP | F_UDP | F_ICMPV4 | F_ICMPV6):
-            raise ValueError("the L4 header starts at or past ZP_L4_FAR (262,143): "
-                             "not representable in the 8-B record")
         if flags & F_TCP:
             p.tcp = TcpReader(frame[l4:])
         if flags & F_UDP:

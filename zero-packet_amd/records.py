@@ -1,8 +1,10 @@
-"""zp_record layout (include/zero_packet.h, ABI v4) as numpy dtypes."""
+"""zp_record layout (include/zero_packet.h, ABI v5) as numpy dtypes."""
 import numpy as np
 
 # The 8-B record: flags (bits 0-23 ZP_F_*, 24-25 Ethernet code, 26-31 err)
 # and offs (bits 0-17 l4_off, 18-31 inner_off). unpack() gives the fields.
+# Far-L4 form (Ethernet code 3): offs is the whole L4 offset; the Ethernet
+# header length and inner_off are read from the frame (decode()).
 RECORD_DTYPE = np.dtype([("flags", "<u4"), ("offs", "<u4")])
 assert RECORD_DTYPE.itemsize == 8
 # unpack()'s per-field view (the final next headers are not in the record:
@@ -10,7 +12,8 @@ assert RECORD_DTYPE.itemsize == 8
 FIELDS_DTYPE = np.dtype([("flags", "<u4"), ("err", "u1"), ("eth_len", "u1"),
                          ("inner_off", "<u4"), ("l4_off", "<u4")])
 F_MASK = 0x00FFFFFF
-L4_FAR = 0x3FFFF          # ZP_L4_FAR: an L4 header at or past this offset
+L4_NEAR_MAX = 0x3FFFF     # ZP_L4_NEAR_MAX: largest l4_off of the ordinary form
+ETH_CODE_FAR = 3          # ZP_ETH_CODE_FAR
 # One IPv6 extension chain (zp_ext_offsets). A batch of n frames has 2n of
 # them: [0, n) the outer ipv6 chains, [n, 2n) the ip_in_ip ones; numpy views
 # them as shape (2, n). final_nh = ExtensionHeaders::final_next_header.
@@ -21,7 +24,9 @@ RECORD_BYTES, EXT_BYTES = 8, 16
 
 
 def unpack(rec):
-    """RECORD_DTYPE array (or raw uint8 [n, 8]) -> FIELDS_DTYPE array."""
+    """RECORD_DTYPE array (or raw uint8 [n, 8]) -> FIELDS_DTYPE array. A
+    far-L4 record gives its whole l4_off and eth_len = inner_off = 0 (they
+    are in the frame, not the record: decode())."""
     rec = np.asarray(rec)
     if rec.dtype != RECORD_DTYPE:
         rec = np.ascontiguousarray(rec, dtype=np.uint8).view(RECORD_DTYPE).reshape(-1)
@@ -30,10 +35,74 @@ def unpack(rec):
     err = w >> 26
     out["err"] = err
     ok = err == 0
+    far = ok & (((w >> 24) & 3) == ETH_CODE_FAR)
+    near = ok & ~far
     out["flags"] = np.where(ok, w & F_MASK, 0)
-    out["eth_len"] = np.where(ok, 14 + 4 * ((w >> 24) & 3), 0)
-    out["l4_off"] = np.where(ok, o & L4_FAR, 0)
-    out["inner_off"] = np.where(ok, o >> 18, 0)
+    out["eth_len"] = np.where(near, 14 + 4 * ((w >> 24) & 3), 0)
+    out["l4_off"] = np.where(near, o & L4_NEAR_MAX, np.where(far, o, 0))
+    out["inner_off"] = np.where(near, o >> 18, 0)
+    return out
+
+
+def is_far(rec):
+    """True where RECORD_DTYPE records hold the far-L4 form."""
+    w = np.asarray(rec["flags"]).astype(np.uint32)
+    return ((w >> 26) == 0) & (((w >> 24) & 3) == ETH_CODE_FAR)
+
+
+def _be16(b, i):
+    return (b[i] << 8) | b[i + 1]
+
+
+def _ipv6_chain(frame, ip, chained, x):
+    """(extension_headers_len, final_next_header) of the IPv6 header at
+    frame[ip:] (ipv6.rs:141, 219-227): from its ext entry x, or its
+    next-header byte without a chain."""
+    if not chained:
+        return 0, frame[ip + 6]
+    if x is None:
+        raise ValueError("the record flags an IPv6 extension chain: pass its ext entries")
+    return int(x["len"]), int(x["final_nh"])
+
+
+def decode(frame, rec, ext=None):
+    """One record of `frame` with every field (zp_rec_decode of
+    include/zero_packet.h restated): dict flags, err, eth_len, inner_off,
+    l4_off, final_nh, inner_final_nh. Both forms; for the far-L4 form the
+    Ethernet header length comes from the frame (ethernet.rs:155-179) and
+    inner_off follows the outer IP header (IPv4 IHL * 4, ipv4.rs:228-258;
+    IPv6 40 + extension_headers_len, ipv6.rs:283-285). ext: the frame's two
+    EXT_DTYPE entries, needed where the record flags a chain."""
+    frame = bytes(frame)
+    w, o = int(rec["flags"]), int(rec["offs"])
+    out = dict(flags=0, err=w >> 26, eth_len=0, inner_off=0, l4_off=0, final_nh=0,
+               inner_final_nh=0)
+    if out["err"]:
+        return out
+    flags = w & F_MASK
+    out["flags"] = flags
+    far = (w >> 24) & 3 == ETH_CODE_FAR
+    l4_any = F_TCP | F_UDP | F_ICMPV4 | F_ICMPV6
+    if far:
+        if not flags & l4_any or not flags & F_IP_IN_IP:
+            raise ValueError("far-L4 record without an L4 reader or an ip_in_ip header")
+        t = _be16(frame, 12)
+        out["eth_len"] = 18 if t == 0x8100 else 22 if t == 0x88A8 else 14
+        out["l4_off"] = o
+    else:
+        out["eth_len"] = 14 + 4 * ((w >> 24) & 3)
+        out["l4_off"] = o & L4_NEAR_MAX
+        out["inner_off"] = o >> 18
+    hl = out["eth_len"]
+    chain = 0
+    if flags & F_IPV6:
+        chain, out["final_nh"] = _ipv6_chain(frame, hl, flags & F_EXT,
+                                             None if ext is None else ext[0])
+    if far:
+        out["inner_off"] = hl + 40 + chain if flags & F_IPV6 else hl + (frame[hl] & 15) * 4
+    if flags & F_IP_IN_IP_V6:
+        out["inner_final_nh"] = _ipv6_chain(frame, out["inner_off"], flags & F_INNER_EXT,
+                                            None if ext is None else ext[1])[1]
     return out
 
 
