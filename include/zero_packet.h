@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define ZP_ABI_VERSION 5   /* 2: 16-B record, extension chains in the ext side array;
+#define ZP_ABI_VERSION 6   /* 2: 16-B record, extension chains in the ext side array;
                               3: reader-accessor error codes 36-37 (ZP_ERR_COUNT 38,
                                  ZP_STATS_COUNT 62), standalone readers and the
                                  checksum primitives (zp_reader_new, zp_*checksum*);
@@ -35,7 +35,10 @@ extern "C" {
                                  final next header of a chain in its ext entry;
                               5: the far-L4 form (Ethernet code 3, the whole L4
                                  offset in `offs`) replaces v4's saturation at
-                                 ZP_L4_FAR; zp_rec_decode */
+                                 ZP_L4_FAR; zp_rec_decode;
+                              6: the inline outer chain (ZP_CHAIN_INLINE): a short
+                                 RFC-ordered IPv6 extension chain of a frame without
+                                 ip_in_ip lives in the record, no ext entry */
 
 /* ------------------------------------------------------------------------- */
 /* Per-packet parse error codes. One code per DISTINCT reference error string */
@@ -165,7 +168,39 @@ static inline int      zp_rec_is_far(zp_record r)  { return ((r.flags >> 24) & 3
 static inline uint32_t zp_rec_l4_off(zp_record r)  { return zp_rec_is_far(r) ? r.offs : r.offs & ZP_L4_NEAR_MAX; }
 /* Ordinary form only (0 for a far-L4 record: zp_rec_decode reads them from the frame). */
 static inline uint32_t zp_rec_eth_len(zp_record r)   { return zp_rec_is_far(r) ? 0u : 14u + 4u * ((r.flags >> 24) & 3u); }
-static inline uint32_t zp_rec_inner_off(zp_record r) { return zp_rec_is_far(r) ? 0u : r.offs >> 18; }
+static inline uint32_t zp_rec_inner_off(zp_record r) {
+    return zp_rec_is_far(r) || !(r.flags & ZP_F_IP_IN_IP) ? 0u : r.offs >> 18;
+}
+
+/*
+ * Inline outer chain (ABI v6). A frame without an ip_in_ip header leaves the
+ * inner_off field (offs bits 18-31) free. When its outer IPv6 extension chain
+ * is short and in RFC 8200 order and the frame has an L4 reader, the chain is
+ * stored there and its ext entry is NOT written (c4-shaped traffic then
+ * writes 8 B per frame instead of 8 + 16):
+ *
+ *   offs bit 31      ZP_CHAIN_INLINE
+ *   offs bits 18-20  Hop-by-Hop  length code c: (c + 1) * 8 B   (options.rs:123)
+ *   offs bits 21-22  Destination 1st         c: (c + 1) * 8 B
+ *   offs bits 23-25  Routing                 c: (c + 1) * 8 B   (routing.rs:164)
+ *   (Fragment: always 8 B, fragment.rs:158)
+ *   offs bits 26-27  Authentication          c: (c + 2) * 4 B   (authentication.rs:173)
+ *   offs bits 28-29  Destination 2nd         c: (c + 1) * 8 B
+ *
+ * The present headers (the record's ZP_F_EXT_SLOT bits) lie back to back in
+ * the order Hop-by-Hop, Destination 1st, Routing, Fragment, Authentication,
+ * Destination 2nd; slot offsets are the running sums, extension_headers_len
+ * the total, and final_next_header (headers.rs:26) the protocol of the
+ * record's L4 reader (6 / 17 / 1 / 58). zp_rec_chain() rebuilds the
+ * zp_ext_offsets entry; the host paths (zp_parse_batch_host, zp_parse_one,
+ * the ring) hand out the rebuilt entry, so only device-batch callers see the
+ * inline form. Any other chain keeps its 16-B entry.
+ */
+#define ZP_CHAIN_INLINE (1u << 31)
+static inline int zp_rec_chain_inline(zp_record r) {
+    return (r.flags >> 26) == 0 && !zp_rec_is_far(r) &&
+           (r.flags & (ZP_F_EXT | ZP_F_IP_IN_IP)) == ZP_F_EXT && (r.offs & ZP_CHAIN_INLINE) != 0;
+}
 
 /*
  * One IPv6 extension chain (Some(ExtensionHeaders), headers.rs:19-28), 16 B:
@@ -174,7 +209,8 @@ static inline uint32_t zp_rec_inner_off(zp_record r) { return zp_rec_is_far(r) ?
  * final_nh = ExtensionHeaders::final_next_header (headers.rs:26).
  *
  * The ext side array of a batch of n frames holds 2n entries:
- *   ext[i]     the outer ipv6 chain of frame i, valid iff flags & ZP_F_EXT;
+ *   ext[i]     the outer ipv6 chain of frame i, valid iff flags & ZP_F_EXT and
+ *              the chain is not inline (zp_rec_chain_inline; device batches only);
  *   ext[n + i] the ip_in_ip IPv6 chain,           valid iff flags & ZP_F_INNER_EXT.
  * Entries whose flag is clear are unspecified (the kernel may leave them
  * untouched or zero them). Passing ext = NULL drops the chains (the records
@@ -186,6 +222,31 @@ typedef struct zp_ext_offsets {
     uint8_t  final_nh;
     uint8_t  reserved;
 } zp_ext_offsets;
+
+/* The zp_ext_offsets entry of an inline outer chain (zp_rec_chain_inline(r)
+ * must hold): slot offsets, extension_headers_len and final_next_header. */
+static inline void zp_rec_chain(zp_record r, zp_ext_offsets* x) {
+    static const uint8_t order[6] = {ZP_EXT_HBH, ZP_EXT_DST1, ZP_EXT_RT, ZP_EXT_FRAG,
+                                     ZP_EXT_AH, ZP_EXT_DST2};
+    const uint32_t c = r.offs >> 18;
+    const uint32_t len[6] = {                         /* by slot                   */
+        ((c & 7u) + 1u) * 8u,                         /* ZP_EXT_HBH,  bits 18-20   */
+        (((c >> 5) & 7u) + 1u) * 8u,                  /* ZP_EXT_RT,   bits 23-25   */
+        8u,                                           /* ZP_EXT_FRAG               */
+        (((c >> 8) & 3u) + 2u) * 4u,                  /* ZP_EXT_AH,   bits 26-27   */
+        (((c >> 3) & 3u) + 1u) * 8u,                  /* ZP_EXT_DST1, bits 21-22   */
+        (((c >> 10) & 3u) + 1u) * 8u};                /* ZP_EXT_DST2, bits 28-29   */
+    uint32_t at = 0;
+    for (int k = 0; k < ZP_EXT_SLOTS; ++k) x->off[k] = 0;
+    for (int j = 0; j < 6; ++j) {
+        const int k = order[j];
+        if (r.flags & ZP_F_EXT_SLOT(k)) { x->off[k] = (uint16_t)at; at += len[k]; }
+    }
+    x->len = (uint16_t)at;
+    x->final_nh = (uint8_t)((r.flags & ZP_F_TCP) ? 6 : (r.flags & ZP_F_UDP) ? 17
+                          : (r.flags & ZP_F_ICMPV4) ? 1 : 58);
+    x->reserved = 0;
+}
 
 /* A record with every field unpacked (PacketParser's readers by start
  * offset): flags = ZP_F_* bits, eth_len 14/18/22, final_nh / inner_final_nh

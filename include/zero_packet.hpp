@@ -445,6 +445,11 @@ struct PacketParser {
                                     const zp_ext_offsets* inner = nullptr) {
         if (zp_rec_err(r)) detail::fail((int)zp_rec_err(r));
         const uint32_t flags = r.flags & ZP_F_MASK;
+        zp_ext_offsets inl{};
+        if (zp_rec_chain_inline(r)) {                 // ABI v6: the outer chain in the record
+            zp_rec_chain(r, &inl);
+            outer = &inl;
+        }
         if (((flags & ZP_F_EXT) && !outer) || ((flags & ZP_F_INNER_EXT) && !inner))
             throw std::invalid_argument("from_record: the record flags an extension chain");
         PacketParser p;

@@ -364,10 +364,50 @@ typedef struct zpo_record {
     uint32_t inner_off, l4_off;
 } zpo_record;
 
+/* The inline code of an outer chain (ZP_CHAIN_INLINE, include/zero_packet.h,
+ * ABI v6) from the record and the chain's entry, or 0 when the chain does not
+ * go inline: the present headers sorted by offset must come in RFC 8200 order
+ * (Hop-by-Hop, Destination 1st, Routing, Fragment, Authentication,
+ * Destination 2nd) with lengths their code fields hold, and the frame needs an
+ * L4 reader and no ip_in_ip header. */
+static uint32_t chain_code(const zpo_record* r, const zp_ext_offsets* x) {
+    static const int rfc[6] = {ZP_EXT_HBH, ZP_EXT_DST1, ZP_EXT_RT, ZP_EXT_FRAG, ZP_EXT_AH,
+                               ZP_EXT_DST2};
+    const uint32_t l4 = ZP_F_TCP | ZP_F_UDP | ZP_F_ICMPV4 | ZP_F_ICMPV6;
+    if (!x || (r->flags & (ZP_F_EXT | ZP_F_IP_IN_IP)) != ZP_F_EXT || !(r->flags & l4) ||
+        r->l4_off > ZP_L4_NEAR_MAX)
+        return 0;
+    int seq[6], m = 0;
+    for (int j = 0; j < 6; ++j)
+        if (r->flags & ZP_F_EXT_SLOT(rfc[j])) seq[m++] = rfc[j];
+    uint32_t code = ZP_CHAIN_INLINE >> 18, at = 0;
+    for (int q = 0; q < m; ++q) {
+        const int k = seq[q];
+        if (x->off[k] != at) return 0;                      /* not in RFC order */
+        const uint32_t end = q + 1 < m ? x->off[seq[q + 1]] : x->len;
+        if (end <= at) return 0;
+        const uint32_t hl = end - at;
+        if (k == ZP_EXT_FRAG) {
+            if (hl != 8) return 0;
+        } else if (k == ZP_EXT_AH) {
+            if (hl % 4 || hl / 4 - 2 > 3) return 0;
+            code |= (hl / 4 - 2) << 8;
+        } else {
+            const uint32_t c = hl / 8 - 1, cmax = (k == ZP_EXT_HBH || k == ZP_EXT_RT) ? 7u : 3u;
+            if (hl % 8 || c > cmax) return 0;
+            code |= c << (k == ZP_EXT_HBH ? 0 : k == ZP_EXT_RT ? 5 : k == ZP_EXT_DST1 ? 3 : 10);
+        }
+        at = end;
+    }
+    return code;
+}
+
 /* zp_record (include/zero_packet.h): flags | Ethernet code << 24 | err << 26,
- * l4_off | inner_off << 18; an l4_off past ZP_L4_NEAR_MAX in the far-L4 form
- * (code 3, offs = l4_off; ABI v5). */
-void zpo_pack(const zpo_record* full, uint64_t n, zp_record* out) {
+ * l4_off | inner_off << 18, or the outer chain's inline code in bits 18-31
+ * (ABI v6; outer = the n outer-chain entries, NULL: no inline chains); an
+ * l4_off past ZP_L4_NEAR_MAX in the far-L4 form (code 3, offs = l4_off; ABI
+ * v5). */
+void zpo_pack(const zpo_record* full, const zp_ext_offsets* outer, uint64_t n, zp_record* out) {
     for (uint64_t i = 0; i < n; ++i) {
         const zpo_record* r = &full[i];
         if (r->err) {
@@ -380,8 +420,9 @@ void zpo_pack(const zpo_record* full, uint64_t n, zp_record* out) {
             out[i].offs = r->l4_off;
             continue;
         }
+        const uint32_t code = chain_code(r, outer ? &outer[i] : NULL);
         out[i].flags = r->flags | ((uint32_t)(r->eth_len - 14) / 4u) << 24;
-        out[i].offs = r->l4_off | r->inner_off << 18;
+        out[i].offs = r->l4_off | (code ? code : r->inner_off) << 18;
     }
 }
 

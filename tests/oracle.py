@@ -40,7 +40,7 @@ def lib():
         l.zpo_pseudo_header.restype = ctypes.c_uint32
         l.zpo_pseudo_header.argtypes = [vp, vp, sz, ctypes.c_uint8, sz]
         l.zpo_pack.restype = None
-        l.zpo_pack.argtypes = [vp, u64, vp]
+        l.zpo_pack.argtypes = [vp, vp, u64, vp]
         _lib = l
     return _lib
 
@@ -56,12 +56,17 @@ def parse_one(frame):
     return err, rec[0], ext
 
 
-def pack(rec):
-    """oracle records (RECORD_DTYPE) -> the ABI's 8-B records (PACKED_DTYPE)."""
+def pack(rec, ext):
+    """oracle records (RECORD_DTYPE) + their chains (EXT_DTYPE (2, n), or (2,)
+    for one record) -> the ABI's 8-B records (PACKED_DTYPE); an outer chain
+    goes inline where the ABI v6 rule says so (zpo_pack)."""
     rec = np.ascontiguousarray(np.atleast_1d(rec), dtype=RECORD_DTYPE)
+    ext = np.asarray(ext, dtype=EXT_DTYPE)
+    outer = np.ascontiguousarray(ext.reshape(2, -1)[0])
+    assert len(outer) == len(rec), "pack: one outer-chain entry per record"
     out = np.zeros(len(rec), PACKED_DTYPE)
     if len(rec):
-        lib().zpo_pack(rec.ctypes.data, len(rec), out.ctypes.data)
+        lib().zpo_pack(rec.ctypes.data, outer.ctypes.data, len(rec), out.ctypes.data)
     return out
 
 
@@ -69,7 +74,7 @@ def parse_one_abi(frame):
     """parse_one with the record packed as the ABI's zp_record (what the GPU
     path returns and the facades' from_record takes)."""
     err, rec, ext = parse_one(frame)
-    return err, pack(rec)[0], ext
+    return err, pack(rec, ext)[0], ext
 
 
 def record_tuple(rec, ext):

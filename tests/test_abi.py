@@ -52,7 +52,7 @@ def test_err_strings(zp):
         35: "IPv6 encapsulated checksum is invalid.",
     }
     lib = zp._lib.hip()
-    assert lib.zp_abi_version() == 5
+    assert lib.zp_abi_version() == 6
     assert lib.zp_err_str(0) == b""
     for code, s in want.items():
         assert lib.zp_err_str(code).decode() == s
@@ -69,7 +69,8 @@ def test_record_layout(zp):
     assert r.fields["flags"][1] == 0 and r.fields["offs"][1] == 4
     assert e.fields["len"][1] == 0 and e.fields["off"][1] == 2 and e.fields["final_nh"][1] == 14
     rec = np.zeros(3, r)
-    rec[0] = (zp.records.F_ETHERNET | zp.records.F_IPV6 | zp.records.F_TCP | 2 << 24, 170 | 150 << 18)
+    rec[0] = (zp.records.F_ETHERNET | zp.records.F_IPV6 | zp.records.F_IP_IN_IP | zp.records.F_TCP |
+              2 << 24, 170 | 150 << 18)
     rec[1] = (29 << 26, 0)                                   # Err(UDP_LENGTH)
     rec[2] = (zp.records.F_ETHERNET | zp.records.F_IPV6 | zp.records.F_IP_IN_IP |
               zp.records.F_UDP | 3 << 24, 264014)              # far-L4 form (ABI v5)
@@ -77,7 +78,8 @@ def test_record_layout(zp):
     assert list(u["err"]) == [0, 29, 0] and list(u["eth_len"]) == [22, 0, 0]
     assert list(u["l4_off"]) == [170, 0, 264014] and list(u["inner_off"]) == [150, 0, 0]
     assert list(zp.records.is_far(rec)) == [False, False, True]
-    assert u["flags"][0] == zp.records.F_ETHERNET | zp.records.F_IPV6 | zp.records.F_TCP
+    assert u["flags"][0] == (zp.records.F_ETHERNET | zp.records.F_IPV6 | zp.records.F_IP_IN_IP |
+                             zp.records.F_TCP)
     assert list(zp.records.rec_err(rec)) == [0, 29, 0]
 
 

@@ -21,7 +21,7 @@ def getter_columns(zp, frame, rec, ext):
     want = {name: (np.zeros(w, dt) if w > 1 else dt(0)) for name, dt, w in orc.COLUMN_SPEC}
     if int(rec["err"]):
         return want
-    p = zp.PacketParser.from_record(frame, orc.pack(rec)[0], ext)   # the ABI record
+    p = zp.PacketParser.from_record(frame, orc.pack(rec, ext)[0], ext)   # the ABI record
     e = p.ethernet
     if e is None:
         return want

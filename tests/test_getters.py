@@ -218,7 +218,7 @@ def test_gpu_columns_return_the_reference_values(zp, golden):
     cols = zp.columns.extract(torch.from_numpy(arena).to(d),
                               torch.from_numpy(offs.astype(np.int64)).to(d),
                               torch.from_numpy(lens.astype(np.int32)).to(d),
-                              torch.from_numpy(orc.pack(rec).view(np.uint8).reshape(-1, 8)).to(d))
+                              torch.from_numpy(orc.pack(rec, np.zeros((2, len(rec)), orc.EXT_DTYPE)).view(np.uint8).reshape(-1, 8)).to(d))
     cols = {k: v.cpu().numpy() for k, v in cols.items()}
     get = lambda c, i: c[i].tolist() if c.ndim > 1 else int(c[i])
     assert _check_columns(frames, cols, get) == 38

@@ -52,7 +52,7 @@ def assert_same(got, got_ext, want, want_ext):
     """Records byte-identical; the extension chains the records flag
     identical (records.ext_match; other ext entries are unspecified)."""
     g = got.view(np.uint8).reshape(-1, 8)
-    w = orc.pack(want).view(np.uint8).reshape(-1, 8)     # the oracle's records, packed
+    w = orc.pack(want, want_ext).view(np.uint8).reshape(-1, 8)   # the oracle's records, packed
     diff = np.nonzero((g != w).any(1))[0]
     assert len(diff) == 0, (f"{len(diff)} records differ; first {diff[:5]}",
                             got[diff[:3]], want[diff[:3]])
@@ -464,14 +464,18 @@ def test_parse_one_threads(zp, golden):
     assert not bad, bad[:5]
 
 
-def test_ext_null_and_sparse(zp):
+def test_ext_null_and_sparse(zp, golden):
     """ext = NULL drops the chains only (records identical); with an ext array
     the flagged chains match the oracle both where a wave holds many chains
     (whole-wave writes) and where it holds one (that entry only); a sentinel
-    shows which entries a sparse wave leaves untouched."""
+    shows which entries a wave leaves untouched. c4's chains are short and in
+    RFC order: they go inline in the record (ABI v6) and their entries are
+    never written; chains behind an ip_in_ip header (or long / out of order)
+    keep their entries."""
     import ctypes
+    R = zp.records
     arena, offs, lens = zp.batch.generate("c4", 4096, device=dev())
-    ext_rich = arena.new_zeros((2, 4096, 16))
+    ext_rich = torch.full((2, 4096, 16), 0xA5, dtype=torch.uint8, device=dev())
     r1, _ = zp.batch.parse_batch(arena, offs, lens, ext=ext_rich)
     r0 = torch.empty_like(r1)
     s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -482,27 +486,41 @@ def test_ext_null_and_sparse(zp):
     want, wext = orc.parse_batch(arena.cpu().numpy(), offs.cpu().numpy(), lens.cpu().numpy())
     got, gext = zp.batch.records_to_numpy(r1, ext_rich)
     assert_same(got, gext, want, wext)
-    # one IPv6 frame with a chain among IPv4 frames: a sparse wave
+    inl = R.chain_inline(got)
+    chained = (want["flags"] & R.F_EXT) != 0
+    assert chained.sum() > 3000 and (inl == chained).all()        # every c4 chain inline
+    assert (ext_rich.cpu().numpy()[0][inl] == 0xA5).all()         # ... and no entry written
+    # chains that keep their entries: behind ip_in_ip / out of RFC order
+    fx = [bytes.fromhex(f["bytes"]) for f in golden["fixtures"]]
+    wide = []
+    for f in fx:
+        err, rec, ext = orc.parse_one(f)
+        if not err and int(rec["flags"]) & R.F_EXT and not R.chain_inline(orc.pack(rec, ext))[0]:
+            wide.append(f)
+    assert wide
     a3, o3, l3 = zp.batch.generate("c3", 127, device=dev())
-    frames = [a3[int(o):int(o) + int(l)].cpu().numpy().tobytes()
-              for o, l in zip(o3.cpu().numpy(), l3.cpu().numpy())]
-    k = int(((want["flags"] & zp.records.F_EXT) != 0).nonzero()[0][0])
-    o4 = offs.cpu().numpy()
-    frames.insert(70, arena[int(o4[k]):int(o4[k]) + int(lens[k])].cpu().numpy().tobytes())
-    a, o, l_ = pack(frames)
+    c3 = [a3[int(o):int(o) + int(l)].cpu().numpy().tobytes()
+          for o, l in zip(o3.cpu().numpy(), l3.cpu().numpy())]
     d = dev()
-    ta = torch.from_numpy(a).to(d)
-    to = torch.from_numpy(o.astype(np.int64)).to(d)
-    tl = torch.from_numpy(l_.astype(np.int32)).to(d)
-    ext = torch.full((2, 128, 16), 0xA5, dtype=torch.uint8, device=d)
-    r, _ = zp.batch.parse_batch(ta, to, tl, ext=ext)
-    want, wext = orc.parse_batch(a, o, l_)
-    got, gext = zp.batch.records_to_numpy(r, ext)
-    assert_same(got, gext, want, wext)
-    assert int(((want["flags"] & zp.records.F_EXT) != 0).sum()) == 1
-    e = ext.cpu().numpy()
-    untouched = [i for i in range(128) if i != 70]
-    assert (e[0, untouched] == 0xA5).all() and (e[1] == 0xA5).all()
+    for frames, k_rich in (([wide[i % len(wide)] for i in range(128)], True),   # dense wave
+                           (c3[:70] + [wide[0]] + c3[70:], False)):            # sparse wave
+        a, o, l_ = pack(frames)
+        ta = torch.from_numpy(a).to(d)
+        to = torch.from_numpy(o.astype(np.int64)).to(d)
+        tl = torch.from_numpy(l_.astype(np.int32)).to(d)
+        ext = torch.full((2, 128, 16), 0xA5, dtype=torch.uint8, device=d)
+        r, _ = zp.batch.parse_batch(ta, to, tl, ext=ext)
+        want, wext = orc.parse_batch(a, o, l_)
+        got, gext = zp.batch.records_to_numpy(r, ext)
+        assert_same(got, gext, want, wext)
+        e = ext.cpu().numpy()
+        flagged = (want["flags"] & R.F_EXT) != 0
+        assert not R.chain_inline(got).any()
+        assert (e[0][flagged] != 0xA5).any(axis=1).all()          # written entries
+        if not k_rich:
+            assert flagged.sum() == 1
+            untouched = [i for i in range(128) if i != 70]
+            assert (e[0, untouched] == 0xA5).all()
 
 
 @pytest.mark.parametrize("cfg", ["c1", "c3"])
@@ -602,7 +620,7 @@ def test_config2_full_batch_exact(zp):
     got, gext = zp.batch.records_to_numpy(recs, ext)
     want, wext = orc.parse_batch(arena.cpu().numpy(), offs.cpu().numpy(), lens.cpu().numpy())
     assert (want["err"] == 0).all() and (lens.cpu().numpy() == 64).all()
-    assert got.tobytes() == orc.pack(want).tobytes()
+    assert got.tobytes() == orc.pack(want, wext).tobytes()
     assert zp.records.ext_match(gext, wext, want)
 
 
@@ -684,7 +702,7 @@ def test_parse_one_sizes(zp):
             rc = lib.zp_parse_one(ctx, ctypes.addressof(buf), len(f), rec.ctypes.data,
                                   ext.ctypes.data)
             err, wrec, wext = orc.parse_one(f)
-            assert rc == err and rec.tobytes() == orc.pack(wrec).tobytes(), (len(f), rc, err)
+            assert rc == err and rec.tobytes() == orc.pack(wrec, wext).tobytes(), (len(f), rc, err)
             assert ext.tobytes() == wext.view(np.uint8).tobytes(), len(f)
     finally:
         lib.zp_ctx_destroy(ctx)

@@ -122,7 +122,7 @@ def test_far_records_decode_exactly(zp):
     for (lv, kw), (frame, l4) in zip(CASES, _cases()):
         err, rec, ext = orc.parse_one(frame)
         assert err == 0 and rec["l4_off"] == l4, (lv, kw, err)
-        packed = orc.pack(rec)[0]
+        packed = orc.pack(rec, ext)[0]
         far = l4 > R.L4_NEAR_MAX
         assert bool(R.is_far(np.array([packed], R.RECORD_DTYPE))[0]) == far
         if far:
@@ -149,7 +149,7 @@ def test_far_record_mismatch_is_refused(zp):
     """zp_rec_decode refuses a far record that cannot belong to the frame."""
     frame, l4 = deep_frame(6600)
     _, rec, ext = orc.parse_one(frame)
-    packed = orc.pack(rec)[0].copy()
+    packed = orc.pack(rec, ext)[0].copy()
     rc, _ = _zp_decode(zp, frame[:l4], packed, ext)        # L4 past the end
     assert rc == -1
     packed["flags"] = int(packed["flags"]) & ~zp.records.F_IP_IN_IP
@@ -175,7 +175,7 @@ def test_l4_far_on_the_gpu(zp):
     want, wext = orc.parse_batch(arena, offs.astype(np.uint64), lens.astype(np.uint32))
     assert (want["err"] == 0).all()
     assert zp.records.is_far(got).sum() == sum(l4 > zp.records.L4_NEAR_MAX for _, l4 in cases)
-    assert got.tobytes() == orc.pack(want).tobytes()
+    assert got.tobytes() == orc.pack(want, wext).tobytes()
     assert zp.records.ext_match(gext, wext, want)
     for k, (f, l4) in enumerate(cases):
         pd = zp.records.decode(f, got[k], gext[:, k])

@@ -24,7 +24,7 @@ def check_expect(zpkg, frame, rec, ext, expect):
     """Evaluates a fixture's transcribed asserts against a record via the
     PacketParser facade (the same check serves oracle and GPU records)."""
     if "err" in rec.dtype.names:                 # the oracle's unpacked record
-        err, rec = int(rec["err"]), orc.pack(rec)[0]
+        err, rec = int(rec["err"]), orc.pack(rec, ext)[0]
     else:                                        # the ABI's 8-B record
         err = int(rec["flags"]) >> 26
     if not expect["ok"]:

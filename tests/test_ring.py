@@ -29,7 +29,7 @@ def test_ring_parse_matches_oracle(zp, cfg, slots, slot_bytes):
     want, wext = orc.parse_batch(arena, offs, lens)
     with zp.ring.Ring(0, slots, slot_bytes) as ring:
         got, gext = ring.parse(arena, offs, lens)
-    assert got.tobytes() == orc.pack(want).tobytes()
+    assert got.tobytes() == orc.pack(want, wext).tobytes()
     assert zp.records.ext_match(gext, wext, want)
 
 
@@ -75,7 +75,9 @@ def test_ring_producer_consumer_threads(zp, golden):
     assert not tp.is_alive() and not tc.is_alive()
     assert sorted(results) == list(range(len(batches)))
     for seq, b in enumerate(batches):
-        want = orc.pack(np.array([orc.parse_one(f)[1] for f in b], orc.RECORD_DTYPE))
+        one = [orc.parse_one(f) for f in b]
+        want = orc.pack(np.array([o[1] for o in one], orc.RECORD_DTYPE),
+                        np.stack([o[2] for o in one], axis=1))
         assert results[seq].tobytes() == want.tobytes(), seq
     ring.close()
 

@@ -21,7 +21,7 @@ for s in "$@"; do
   i=$((i+1))
   case $s in
     build)  step build 600 python __graft_entry__.py ;;
-    tests)  step gpu_tests 1200 python -m pytest tests -m gpu -q -p no:cacheprovider --timeout 600 ;;
+    tests)  step gpu_tests 1200 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     smoke)  step smoke 300 python __graft_entry__.py smoke ;;
     bench)  step bench 900 python bench.py ;;
     prof)   step prof 900 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --no-pcie ;;

@@ -269,3 +269,56 @@ extern "C" int membw_copy_tiles(const void* src, void* dst, uint64_t bytes, uint
                        (const uint8_t*)src, (uint8_t*)dst, region);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+
+// FETCH_SIZE calibration by access width (the builder's dword
+// blob loads were never calibrated). Every byte of the buffer read exactly
+// once, coalesced, grid-stride, W bytes per lane per load (W = 4, 8, 16);
+// STRIDE5: the builder's blob pattern (each lane 5 aligned dwords from its
+// own 16-B chunk, adjacent lanes adjacent chunks: every byte read by one or
+// two lanes, every line once from HBM).
+template <int W>
+__global__ void __launch_bounds__(256) read_width(const uint8_t* __restrict__ p, uint64_t n,
+                                                  uint32_t* __restrict__ out) {
+    uint32_t acc = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n / W; i += stride) {
+        if constexpr (W == 4) {
+            acc += __builtin_nontemporal_load((const uint32_t*)p + i);
+        } else if constexpr (W == 8) {
+            typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+            const u32x2 v = __builtin_nontemporal_load((const u32x2*)p + i);
+            acc += v.x ^ v.y;
+        } else {
+            typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+            const u32x4 v = __builtin_nontemporal_load((const u32x4*)p + i);
+            acc += v.x ^ v.y ^ v.z ^ v.w;
+        }
+    }
+    if (acc == 0x9E3779B9u) out[blockIdx.x] = acc;
+}
+
+__global__ void __launch_bounds__(256) read_stride5(const uint8_t* __restrict__ p, uint64_t n,
+                                                    uint32_t* __restrict__ out) {
+    uint32_t acc = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    const uint32_t* d = (const uint32_t*)p;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i + 1 < n / 16; i += stride) {
+        uint32_t v[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) v[k] = d[4 * i + k];
+        acc += __builtin_amdgcn_alignbyte(v[1], v[0], 1) ^ v[2] ^ v[3] ^ v[4];
+    }
+    if (acc == 0x9E3779B9u) out[blockIdx.x] = acc;
+}
+
+extern "C" int membw_width(const void* p, uint64_t bytes, uint32_t* out, int width, int blocks,
+                           void* stream) {
+    const uint8_t* q = (const uint8_t*)p;
+    hipStream_t s = (hipStream_t)stream;
+    if (width == 4) hipLaunchKernelGGL(read_width<4>, dim3(blocks), dim3(256), 0, s, q, bytes, out);
+    else if (width == 8) hipLaunchKernelGGL(read_width<8>, dim3(blocks), dim3(256), 0, s, q, bytes, out);
+    else if (width == 16) hipLaunchKernelGGL(read_width<16>, dim3(blocks), dim3(256), 0, s, q, bytes, out);
+    else if (width == 5) hipLaunchKernelGGL(read_stride5, dim3(blocks), dim3(256), 0, s, q, bytes, out);
+    else return -1;
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}

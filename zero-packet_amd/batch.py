@@ -21,7 +21,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .records import EXT_BYTES, EXT_DTYPE, RECORD_BYTES, RECORD_DTYPE
+from .records import EXT_BYTES, EXT_DTYPE, RECORD_BYTES, RECORD_DTYPE, expand_ext
 
 CONFIGS = {"c1": 1, "c2": 2, "c3": 3, "c4": 4, "c5": 5, "c6": 6}
 SEED = 0x5EED2025
@@ -158,10 +158,12 @@ def record_flags(records):
 
 def records_to_numpy(records, ext=None):
     """uint8 [n, 8] (device or host) -> structured numpy (RECORD_DTYPE) [n];
-    with ext (uint8 [2, n, 16]) also the chains as EXT_DTYPE [2, n]."""
+    with ext (uint8 [2, n, 16]) also the chains as EXT_DTYPE [2, n], the
+    entries of inline outer chains (ABI v6, include/zero_packet.h) rebuilt
+    from their records, so every entry a record flags is valid."""
     r = records.cpu().numpy() if isinstance(records, torch.Tensor) else records
     rec = np.ascontiguousarray(r).view(RECORD_DTYPE).reshape(-1)
     if ext is None:
         return rec
     e = ext.cpu().numpy() if isinstance(ext, torch.Tensor) else ext
-    return rec, np.ascontiguousarray(e).view(EXT_DTYPE).reshape(2, -1)
+    return rec, expand_ext(rec, np.ascontiguousarray(e).view(EXT_DTYPE).reshape(2, -1))

@@ -23,7 +23,17 @@ struct zp_rec_full {
     uint32_t flags;
     uint8_t err, eth_len, final_nh, inner_final_nh;
     uint32_t inner_off, l4_off;
+    uint32_t chain;      // the outer chain's inline code (offs bits 18-31), 0: none
 };
+
+// The outer chain goes inline (ZP_CHAIN_INLINE, include/zero_packet.h): the
+// walk found it short and in RFC order, there is no ip_in_ip header and an
+// L4 reader gives final_next_header.
+__device__ __forceinline__ bool zp_chain_inline(const zp_rec_full& r) {
+    return (r.flags & (ZP_F_EXT | ZP_F_IP_IN_IP)) == ZP_F_EXT &&
+           (r.flags & (ZP_F_TCP | ZP_F_UDP | ZP_F_ICMPV4 | ZP_F_ICMPV6)) &&
+           (r.chain & (ZP_CHAIN_INLINE >> 18)) && r.l4_off <= ZP_L4_NEAR_MAX;
+}
 
 // The 8-B record (include/zero_packet.h); an L4 reader past ZP_L4_NEAR_MAX
 // takes the far-L4 form: Ethernet code 3, the whole offset in `offs`.
@@ -31,7 +41,8 @@ __device__ __forceinline__ zp_u32x2 zp_pack(const zp_rec_full& r) {
     if (r.err) return zp_u32x2{(uint32_t)r.err << 26, 0u};
     const bool far = r.l4_off > ZP_L4_NEAR_MAX;
     const uint32_t code = far ? ZP_ETH_CODE_FAR : (uint32_t)(r.eth_len - 14) >> 2;
-    return zp_u32x2{r.flags | code << 24, far ? r.l4_off : r.l4_off | (r.inner_off << 18)};
+    const uint32_t hi = zp_chain_inline(r) ? r.chain : r.inner_off;
+    return zp_u32x2{r.flags | code << 24, far ? r.l4_off : r.l4_off | (hi << 18)};
 }
 
 // A reader R gives frame byte x as rd(x), and bytes [x, x + 4) as one

@@ -167,9 +167,10 @@ static int drain(zp_ctx* c, int k, Pending& pd, zp_record* recs, zp_ext_offsets*
     if (!rec_direct) memcpy(recs + pd.i, c->h_rec[k], m * sizeof(zp_record));
     if (xo) {
         for (uint64_t q = 0; q < m; ++q) {
-            const uint32_t f = recs[pd.i + q].flags;
-            if (f & ZP_F_EXT) xo[pd.i + q] = c->h_ext[k][q];
-            if (f & ZP_F_INNER_EXT) xi[pd.i + q] = c->h_ext[k][m + q];
+            const zp_record r = recs[pd.i + q];
+            if (zp_rec_chain_inline(r)) zp_rec_chain(r, &xo[pd.i + q]);   // ABI v6
+            else if (r.flags & ZP_F_EXT) xo[pd.i + q] = c->h_ext[k][q];
+            if (r.flags & ZP_F_INNER_EXT) xi[pd.i + q] = c->h_ext[k][m + q];
         }
     }
     pd.live = false;
@@ -326,7 +327,8 @@ extern "C" int zp_parse_one(zp_ctx* c, const uint8_t* frame, uint64_t len,
         // entries are defined only where the record flags them (zero_packet.h)
         const zp_ext_offsets* x = (const zp_ext_offsets*)(c->one_h + ONE_EXT);
         memset(ext, 0, 2 * sizeof(zp_ext_offsets));
-        if (record->flags & ZP_F_EXT) ext[0] = x[0];
+        if (zp_rec_chain_inline(*record)) zp_rec_chain(*record, &ext[0]);   // ABI v6
+        else if (record->flags & ZP_F_EXT) ext[0] = x[0];
         if (record->flags & ZP_F_INNER_EXT) ext[1] = x[1];
     }
     return (int)zp_rec_err(*record);

@@ -125,7 +125,8 @@ zp_columns_kernel(const uint8_t* __restrict__ arena, const uint64_t* __restrict_
     const bool far = ((q.x >> 24) & 3u) == ZP_ETH_CODE_FAR;
     r.eth_len = (uint8_t)(far ? 22u : 14u + 4u * ((q.x >> 24) & 3u));
     r.l4_off = far ? q.y : q.y & ZP_L4_NEAR_MAX;
-    r.inner_off = far ? 0u : q.y >> 18;
+    r.inner_off = far || !(r.flags & ZP_F_IP_IN_IP) ? 0u : q.y >> 18;   // else: an inline chain
+    r.chain = 0;
     const bool ok = live && r.err == 0 && (r.flags & ZP_F_ETHERNET);
     const uint32_t len = ok ? lens[i] : 0u;
     const uintptr_t ga = (uintptr_t)arena + (ok ? offs[i] : 0);

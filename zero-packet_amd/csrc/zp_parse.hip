@@ -397,11 +397,14 @@ __device__ __forceinline__ void put_off(uint32_t (&ed)[4], int slot, uint32_t v)
 
 // Extension-header walk (headers.rs:51-213). Returns 0 or a zp_err.
 // pos = IPv6 payload start; outputs slot offsets relative to pos (put_off).
+// *code: the chain's inline code (ZP_CHAIN_INLINE, include/zero_packet.h)
+// when its headers come in RFC order with lengths the code holds, else 0.
 __device__ __forceinline__ int ext_walk(FrameView& f, uint32_t pos, uint32_t nh,
                         uint32_t* present, uint32_t (&ed)[4], uint32_t* total,
-                        uint32_t* final_nh) {
+                        uint32_t* final_nh, uint32_t* code) {
     uint32_t pres = 0, tot = 0, fin = 0;
     uint32_t cur = nh, p = pos;
+    uint32_t cd = ZP_CHAIN_INLINE >> 18, rk = 0;       // rk: RFC rank of the last header + 1
     // One instruction stream for the five header types (Hop-by-Hop :90-113,
     // Routing :117-134, Fragment :138-155, Authentication :159-176,
     // Destination :180-202): a wave whose frames sit on different types runs
@@ -428,6 +431,13 @@ __device__ __forceinline__ int ext_walk(FrameView& f, uint32_t pos, uint32_t nh,
                        : ZP_ERR_EXT_AUTH_EXCEEDS;
         const int slot = hbh ? ZP_EXT_HBH : rt ? ZP_EXT_RT : fr ? ZP_EXT_FRAG : ah ? ZP_EXT_AH
                        : (bit == 32u ? ZP_EXT_DST2 : ZP_EXT_DST1);
+        // inline code: RFC 8200 order HBH, Dest 1st, Routing, Fragment, AH,
+        // Dest 2nd (rank 1..6), each length within its code field
+        const uint32_t rank = hbh ? 1u : rt ? 3u : fr ? 4u : ah ? 5u : bit == 32u ? 6u : 2u;
+        const uint32_t cmax = (hbh || rt) ? 7u : fr ? 0u : 3u;
+        const uint32_t sh = hbh ? 0u : rt ? 5u : ah ? 8u : bit == 32u ? 10u : 3u;
+        cd = (rank > rk && (fr || b1 <= cmax)) ? cd | (fr ? 0u : b1 << sh) : 0u;
+        rk = rank;
         pres |= bit;
         put_off(ed, slot, p - pos);
         tot += hl;
@@ -438,6 +448,7 @@ __device__ __forceinline__ int ext_walk(FrameView& f, uint32_t pos, uint32_t nh,
     *present = pres;
     *total = tot;
     *final_nh = fin;
+    *code = cd;
     return 0;
 }
 
@@ -495,10 +506,10 @@ __device__ __forceinline__ void walk_frame(FrameView& f, Walk& w) {
                     else if (level == 1) { r.flags |= ZP_F_IP_IN_IP; r.inner_off = pos; }
                 } else {                                              // parser.rs:222-230
                     if (sl < 40) { err = ZP_ERR_IPV6_TOO_SHORT; goto done; }
-                    uint32_t pres = 0, tot = 0, fin = 0;
+                    uint32_t pres = 0, tot = 0, fin = 0, cd = 0;
                     uint32_t eo[4] = {0, 0, 0, 0};
                     const uint32_t nh = rd8(f, pos + 6);
-                    const int e = ext_walk(f, pos + 40, nh, &pres, eo, &tot, &fin);  // ipv6.rs:159
+                    const int e = ext_walk(f, pos + 40, nh, &pres, eo, &tot, &fin, &cd);  // ipv6.rs:159
                     if (e) { err = e; goto done; }
                     if ((rd8(f, pos) >> 4) != 6) { err = ZP_ERR_IPV6_VERSION; goto done; }
                     proto = pres ? fin : nh;                          // ipv6.rs:219-227
@@ -508,6 +519,7 @@ __device__ __forceinline__ void walk_frame(FrameView& f, Walk& w) {
                         r.final_nh = (uint8_t)proto;
                         if (pres) {
                             r.flags |= ZP_F_EXT | (pres << 12);
+                            r.chain = cd;
                             // final_next_header (headers.rs:26) in byte 14
                             w.outer = make_uint4(eo[0] | tot, eo[1], eo[2], eo[3] | (proto << 16));
                         }
@@ -940,7 +952,9 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
         // the flagged entries is faster up to k = 24 (-2.4 %), equal at 32,
         // slower from 48 (c4, 56 per wave: +3 %). Nontemporal like the
         // records (c4 -1.3 %, c6 -2.1 %).
-        const bool ho = rec.flags & ZP_F_EXT, hi = rec.flags & ZP_F_INNER_EXT;
+        // an inline outer chain (ABI v6) has no entry
+        const bool ho = (rec.flags & ZP_F_EXT) && !zp_chain_inline(rec),
+                   hi = rec.flags & ZP_F_INNER_EXT;
         const uint64_t mo = __ballot(ho), mi = __ballot(hi);
         if (mo && (ho || __builtin_popcountll(mo) >= ZP_EXT_DENSE))
             store_ext(ext, p, ho ? w.outer : make_uint4(0, 0, 0, 0));

@@ -205,7 +205,10 @@ int zp_rec_decode(const zp_record* rec, const uint8_t* frame, uint64_t len,
     }
     const uint64_t hl = out->eth_len;
     if (flags & ZP_F_IPV6) {
-        if (ipv6_chain(frame, len, hl, (flags & ZP_F_EXT) != 0, ext ? &ext[0] : NULL,
+        zp_ext_offsets inl;
+        const int il = zp_rec_chain_inline(r);                    /* ABI v6 */
+        if (il) zp_rec_chain(r, &inl);
+        if (ipv6_chain(frame, len, hl, (flags & ZP_F_EXT) != 0, il ? &inl : ext ? &ext[0] : NULL,
                        &outer_chain, &out->final_nh))
             return -1;
     }

@@ -284,6 +284,10 @@ extern "C" int zp_ring_wait(zp_ring* r, zp_ring_slot* out, int64_t timeout_ms) {
         RING_ERR("zp_ring_wait: %s", hipGetErrorString(e));
         return -2;
     }
+    // inline outer chains (ABI v6) get their entry rebuilt, so every entry a
+    // record flags is valid for the consumer
+    for (uint64_t i = 0; i < s.n; ++i)
+        if (zp_rec_chain_inline(s.h_rec[i])) zp_rec_chain(s.h_rec[i], &s.h_ext[i]);
     pthread_mutex_lock(&r->mu);
     s.state = S_DONE;
     r->done_head = (k + 1) % r->nslots;

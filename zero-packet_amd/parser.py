@@ -508,6 +508,9 @@ class PacketParser:
             raise ZeroPacketError(_lib.hip().zp_err_str(err).decode() if _lib_available()
                                   else f"zp_err {err}", err)
         flags = word & _rec.F_MASK
+        if _rec.chain_inline(rec):                 # ABI v6: the outer chain in the record
+            ext = _rec.expand_ext(np.array([(rec["flags"], rec["offs"])], RECORD_DTYPE),
+                                  np.zeros(2, EXT_DTYPE) if ext is None else ext).reshape(2)
         if flags & (F_EXT | F_INNER_EXT) and ext is None:
             raise ValueError("the record flags an IPv6 extension chain: pass its ext entries")
         # both record forms (the far-L4 one reads eth_len / inner_off from the frame)

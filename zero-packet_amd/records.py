@@ -40,8 +40,55 @@ def unpack(rec):
     out["flags"] = np.where(ok, w & F_MASK, 0)
     out["eth_len"] = np.where(near, 14 + 4 * ((w >> 24) & 3), 0)
     out["l4_off"] = np.where(near, o & L4_NEAR_MAX, np.where(far, o, 0))
-    out["inner_off"] = np.where(near, o >> 18, 0)
+    out["inner_off"] = np.where(near & ((w & F_IP_IN_IP) != 0), o >> 18, 0)
     return out
+
+
+CHAIN_INLINE = 1 << 31     # ZP_CHAIN_INLINE (offs bit 31, ABI v6)
+_RFC_SLOTS = (0, 4, 1, 2, 3, 5)   # HBH, DST1, RT, FRAG, AH, DST2 (slot numbers)
+
+
+def chain_inline(rec):
+    """True where RECORD_DTYPE records carry their outer IPv6 extension chain
+    inline (zp_rec_chain_inline, include/zero_packet.h): no ext entry."""
+    w = np.asarray(rec["flags"]).astype(np.uint32)
+    o = np.asarray(rec["offs"]).astype(np.uint32)
+    return (((w >> 26) == 0) & (((w >> 24) & 3) != ETH_CODE_FAR) &
+            ((w & (F_EXT | F_IP_IN_IP)) == F_EXT) & ((o & CHAIN_INLINE) != 0))
+
+
+def inline_chains(rec):
+    """zp_rec_chain of every record (EXT_DTYPE [n]; meaningful where
+    chain_inline): headers back to back in RFC order, lengths from the
+    offs bits 18-29, final_next_header from the L4 reader."""
+    rec = np.atleast_1d(rec)
+    w = rec["flags"].astype(np.uint32)
+    c = rec["offs"].astype(np.uint32) >> 18
+    hl = {0: ((c & 7) + 1) * 8, 1: (((c >> 5) & 7) + 1) * 8, 2: np.full_like(c, 8),
+          3: (((c >> 8) & 3) + 2) * 4, 4: (((c >> 3) & 3) + 1) * 8,
+          5: (((c >> 10) & 3) + 1) * 8}
+    out = np.zeros(len(rec), EXT_DTYPE)
+    at = np.zeros(len(rec), np.uint32)
+    for k in _RFC_SLOTS:
+        has = (w & F_EXT_SLOT(k)) != 0
+        out["off"][:, k] = np.where(has, at, 0)
+        at = at + np.where(has, hl[k], 0)
+    out["len"] = at
+    out["final_nh"] = np.where(w & F_TCP, 6, np.where(w & F_UDP, 17,
+                               np.where(w & F_ICMPV4, 1, 58)))
+    return out
+
+
+def expand_ext(rec, ext):
+    """ext (EXT_DTYPE (2, n)) with the entries of inline outer chains rebuilt
+    from their records: every entry a record flags is then valid, as the host
+    paths (zp_parse_batch_host, zp_parse_one, the ring) deliver them."""
+    rec = np.atleast_1d(rec)
+    ext = np.array(ext, dtype=EXT_DTYPE).reshape(2, -1)
+    m = chain_inline(rec)
+    if m.any():
+        ext[0][m] = inline_chains(rec[m])
+    return ext
 
 
 def is_far(rec):
@@ -92,12 +139,13 @@ def decode(frame, rec, ext=None):
     else:
         out["eth_len"] = 14 + 4 * ((w >> 24) & 3)
         out["l4_off"] = o & L4_NEAR_MAX
-        out["inner_off"] = o >> 18
+        out["inner_off"] = o >> 18 if flags & F_IP_IN_IP else 0
     hl = out["eth_len"]
     chain = 0
     if flags & F_IPV6:
-        chain, out["final_nh"] = _ipv6_chain(frame, hl, flags & F_EXT,
-                                             None if ext is None else ext[0])
+        x = inline_chains(np.array([(w, o)], RECORD_DTYPE))[0] \
+            if chain_inline(np.array([(w, o)], RECORD_DTYPE))[0] else (None if ext is None else ext[0])
+        chain, out["final_nh"] = _ipv6_chain(frame, hl, flags & F_EXT, x)
     if far:
         out["inner_off"] = hl + 40 + chain if flags & F_IPV6 else hl + (frame[hl] & 15) * 4
     if flags & F_IP_IN_IP_V6:
