@@ -5,7 +5,9 @@
     lens   int32  [n]       frame lengths (read as uint32)
     -> records uint8 [n, 8] (zp_record), ext uint8 [2, n, 16] (zp_ext_offsets:
        [0] the outer ipv6 extension chains, [1] the ip_in_ip ones; an entry
-       is valid where the record's ZP_F_EXT / ZP_F_INNER_EXT bit is set)
+       is valid where the record's ZP_F_EXT / ZP_F_INNER_EXT bit is set,
+       except an inline outer chain (ABI v6), which lives in its record:
+       records_to_numpy rebuilds those entries)
 
 parse_batch() enqueues the HIP kernel on torch's current stream of the
 tensors' device, or on `stream` (zp_parse_batch_device). By default

@@ -635,17 +635,31 @@ __device__ __forceinline__ uint32_t wbe16(const FrameView& f, uint32_t x) {
     const uint32_t t = __builtin_amdgcn_alignbyte(win_dw(f, d + 1), win_dw(f, d), y & 3);
     return ((t & 0xFFu) << 8) | ((t >> 8) & 0xFFu);
 }
-// Probe: the frame looks like the common shape (two window reads).
-__device__ __forceinline__ bool v4_probe(const FrameView& f) {
-    return f.len >= 64 && wbe16(f, 12) == 0x0800 && wb8(f, 14) == 0x45;
+// The first header fields every straight-line path tests, read from the
+// window once per frame (ethernet.rs:155-179: the tag types, the header
+// length, the ethertype; the IP version / IHL byte and the IPv6 next header).
+struct Probe { uint32_t t0, t1, hl, et, b0, p6; };
+__device__ __forceinline__ Probe probe_frame(const FrameView& f) {
+    Probe p;
+    p.t0 = wbe16(f, 12);
+    p.t1 = wbe16(f, 16);
+    p.hl = p.t0 == 0x8100 ? 18u : p.t0 == 0x88A8 ? 22u : 14u;
+    p.et = wbe16(f, p.hl - 2);
+    p.b0 = wb8(f, p.hl);
+    p.p6 = wb8(f, p.hl + 6);
+    return p;
 }
-__device__ __forceinline__ bool fast_v4(const FrameView& f, Walk& w) {
+// The frame looks like the common shape (untagged Ethernet II, IPv4 IHL 5).
+__device__ __forceinline__ bool v4_probe(const FrameView& f, const Probe& p) {
+    return f.len >= 64 && p.t0 == 0x0800 && p.b0 == 0x45;
+}
+__device__ __forceinline__ bool fast_v4(const FrameView& f, const Probe& pr, Walk& w) {
     const uint32_t len = f.len;
     const uint32_t hv = wsum4<5>(f, 14 + f.shift);                  // ipv4.rs:262-264
     const uint32_t proto = wb8(f, 23);
     const bool tcp = proto == 6, udp = proto == 17, ic4 = proto == 1;
     const uint32_t t = wbe16(f, tcp ? 46u : udp ? 38u : 34u);       // one L4 word
-    bool ok = v4_probe(f) && wbe16(f, 16) == len - 14 &&            // parser.rs:188-212
+    bool ok = v4_probe(f, pr) && pr.t1 == len - 14 &&              // parser.rs:188-212
               hv != 0 && hv % 65535u == 0 && (tcp || udp || ic4);
     ok = ok && (tcp ? (t >> 12) >= 5 && (t & 0xFFu) != 0             // parser.rs:237-247
               : udp ? t == len - 34                                  // parser.rs:258-263
@@ -709,20 +723,17 @@ __device__ __forceinline__ IpLevel ip_level(const FrameView& f, uint32_t pos, bo
 // surely cannot take (ARP, IPv4 options, IPv6 extension headers, runts)
 // skips it, since the general walk then runs for the wave anyway (c6 +1.5 %
 // without this gate).
-__device__ __forceinline__ bool fast_ip_probe(const FrameView& f) {
+__device__ __forceinline__ bool fast_ip_probe(const FrameView& f, const Probe& p) {
     if (f.len < 64) return false;
-    const uint32_t t0 = wbe16(f, 12);
-    const uint32_t hl = t0 == 0x8100 ? 18u : t0 == 0x88A8 ? 22u : 14u;
-    const uint32_t et = wbe16(f, hl - 2), b0 = wb8(f, hl), p6 = wb8(f, hl + 6);
-    const bool ext6 = p6 == 0 || p6 == 43 || p6 == 44 || p6 == 51 || p6 == 60;
-    return et == 0x0800 ? b0 == 0x45 : et == 0x86DD && !ext6;
+    const bool ext6 = p.p6 == 0 || p.p6 == 43 || p.p6 == 44 || p.p6 == 51 || p.p6 == 60;
+    return p.et == 0x0800 ? p.b0 == 0x45 : p.et == 0x86DD && !ext6;
 }
-__device__ __forceinline__ bool fast_ip(FrameView& f, Walk& w) {
+__device__ __forceinline__ bool fast_ip(FrameView& f, const Probe& pr, Walk& w) {
     const uint32_t len = f.len;
     if (len < 64 || len > ZP_GIANT) return false;
-    const uint32_t t0 = wbe16(f, 12), t1 = wbe16(f, 16);                // ethernet.rs:155-179
-    const uint32_t hl = t0 == 0x8100 ? 18u : t0 == 0x88A8 ? 22u : 14u;
-    const uint32_t et = wbe16(f, hl - 2);                               // ethernet.rs:209-212
+    const uint32_t t0 = pr.t0, t1 = pr.t1;                              // ethernet.rs:155-179
+    const uint32_t hl = pr.hl;
+    const uint32_t et = pr.et;                                          // ethernet.rs:209-212
     const bool v4o = et == 0x0800;
     bool ok = (t0 != 0x88A8 || t1 == 0x8100) && (v4o || et == 0x86DD);
     const IpLevel L0 = ip_level(f, hl, v4o);                            // parse_ipv4 / parse_ipv6
@@ -878,12 +889,15 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
     w.rec.flags = ZP_F_ETHERNET;
 #else
     bool done = false;
+#if ZP_FAST_V4 || ZP_FAST_IP
+    const Probe pr = probe_frame(fv);          // the first header fields, read once
+#endif
 #if ZP_FAST_V4
     // The common shape straight-line when most of the wave has it
     // (wave-uniform test); the rest of the frames take the general walk.
-    const bool probe = s.live && v4_probe(fv);
+    const bool probe = s.live && v4_probe(fv, pr);
     if (__builtin_popcountll(__ballot(probe)) >= 32) {
-        if (probe) done = fast_v4(fv, w);
+        if (probe) done = fast_v4(fv, pr, w);
     }
 #endif
 #if ZP_FAST_IP
@@ -891,8 +905,8 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
     // general walk.
     {
         const bool todo = s.live && !done;
-        if (__ballot(todo) && !__ballot(todo && !fast_ip_probe(fv))) {
-            if (todo) done = fast_ip(fv, w);
+        if (__ballot(todo) && !__ballot(todo && !fast_ip_probe(fv, pr))) {
+            if (todo) done = fast_ip(fv, pr, w);
         }
     }
 #endif
