@@ -77,7 +77,8 @@ def test_ring_producer_consumer_threads(zp, golden):
     for seq, b in enumerate(batches):
         one = [orc.parse_one(f) for f in b]
         want = orc.pack(np.array([o[1] for o in one], orc.RECORD_DTYPE),
-                        np.stack([o[2] for o in one], axis=1))
+                        np.stack([o[2] for o in one], axis=1) if one
+                        else np.zeros((2, 0), orc.EXT_DTYPE))
         assert results[seq].tobytes() == want.tobytes(), seq
     ring.close()
 

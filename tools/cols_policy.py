@@ -1,0 +1,89 @@
+"""Fused parse + columns vs parse then columns, by requested column bytes per
+frame (the threshold ZP_FUSED_MAX_COL_BYTES of zp_parse_batch_columns_device):
+tools/variants/libzc_fused.so (threshold 1000: always fused) against
+libzc_split.so (threshold 0: always two kernels), interleaved in one process.
+Usage: python tools/cols_policy.py [--configs c3,c5]"""
+import argparse
+import ctypes
+import importlib
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+SETS = {
+    "ports+proto(5B)": ["protocol", "src_port", "dest_port"],
+    "5tuple(37B)": ["src_addr", "dest_addr", "protocol", "src_port", "dest_port"],
+    "5tuple+l4(47B)": ["src_addr", "dest_addr", "protocol", "src_port", "dest_port", "tcp_seq",
+                       "tcp_ack", "tcp_flags", "l4_proto"],
+    "l3l4(55B)": ["src_addr", "dest_addr", "protocol", "src_port", "dest_port", "tcp_seq",
+                  "tcp_ack", "tcp_flags", "l4_proto", "ttl", "tos", "ip_id", "ip_len",
+                  "ip_version"],
+    "macs+l3l4(67B)": ["dest_mac", "src_mac", "src_addr", "dest_addr", "protocol", "src_port",
+                       "dest_port", "tcp_seq", "tcp_ack", "tcp_flags", "l4_proto", "ttl", "tos",
+                       "ip_id", "ip_len", "ip_version"],
+    "all(73B)": None,
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="c3,c5")
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--rounds", type=int, default=3)
+    a = ap.parse_args()
+    zp = importlib.import_module("zero-packet_amd")
+    C = zp.columns
+    vp, u64 = ctypes.c_void_p, ctypes.c_uint64
+    libs = []
+    for v in ("fused", "split"):
+        l = ctypes.CDLL(os.path.join(ROOT, "tools", "variants", f"libzc_{v}.so"))
+        l.zp_parse_batch_columns_device.argtypes = [vp, vp, vp, u64, vp, vp, vp, vp]
+        libs.append((v, l))
+    d = torch.device("cuda:0")
+    s = torch.cuda.current_stream(d)
+    for cfg in a.configs.split(","):
+        n = {"c3": 1 << 24, "c4": 1 << 24, "c5": 1 << 25}[cfg]
+        arena, offs, lens = zp.batch.generate(cfg, n, device=d)
+        rec = torch.empty((n, 8), dtype=torch.uint8, device=d)
+        ext = torch.empty((2, n, 16), dtype=torch.uint8, device=d)
+        for label, names in SETS.items():
+            names = names or C.NAMES
+            out = {k: C._alloc(k, n, d) for k in names}
+            ptrs = (ctypes.c_void_p * len(C.NAMES))()
+            for k in names:
+                ptrs[C.INDEX[k]] = out[k].data_ptr()
+            width = sum(C.width(k) for k in names)
+            res = {v: [] for v, _ in libs}
+            ref = None
+            for r in range(a.rounds):
+                for v, l in libs:
+                    fn = lambda l=l: l.zp_parse_batch_columns_device(
+                        arena.data_ptr(), offs.data_ptr(), lens.data_ptr(), n, rec.data_ptr(),
+                        ext.data_ptr(), ptrs, s.cuda_stream)
+                    assert fn() == 0
+                    ev = [(torch.cuda.Event(enable_timing=True),
+                           torch.cuda.Event(enable_timing=True)) for _ in range(a.reps)]
+                    for x, y in ev:
+                        x.record(s); fn(); y.record(s)
+                    torch.cuda.synchronize()
+                    res[v] += [x.elapsed_time(y) for x, y in ev]
+                    got = torch.cat([out[k].view(-1) for k in names] + [rec.view(-1)])
+                    if ref is None:
+                        ref = got.clone()
+                    elif not torch.equal(ref, got):
+                        print(f"  !! {cfg} {label} {v}: results differ", flush=True)
+            f, sp = (float(np.median(res[v])) for v in ("fused", "split"))
+            print(f"{cfg} {label:18s} {width:3d} B/frame: fused {f:7.3f} ms  split {sp:7.3f} ms  "
+                  f"fused/split {f / sp:5.3f}", flush=True)
+            del out
+        del arena, offs, lens, rec, ext
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

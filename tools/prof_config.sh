@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 C=${1:-c3}; shift
 O=gpurun_out/prof_$C
 mkdir -p $O
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O -o run --output-format csv -- python3 bench.py --config $C --no-pcie --no-cpu "$@" > $O/bench.log 2>&1 || exit $?
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O -o run --output-format csv -- python3 bench.py --config $C --no-pcie --no-cpu --no-c5 "$@" > $O/bench.log 2>&1 || exit $?
 grep '^{' $O/bench.log > $O/bench.json
 f=$(find $O -name "*kernel_stats.csv" | head -1); cp "$f" $O/kernel_stats.csv
 head -3 $O/kernel_stats.csv
