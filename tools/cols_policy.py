@@ -72,7 +72,7 @@ def main():
                         x.record(s); fn(); y.record(s)
                     torch.cuda.synchronize()
                     res[v] += [x.elapsed_time(y) for x, y in ev]
-                    got = torch.cat([out[k].view(-1) for k in names] + [rec.view(-1)])
+                    got = torch.cat([out[k].view(-1).view(torch.uint8) for k in names] + [rec.view(-1)])
                     if ref is None:
                         ref = got.clone()
                     elif not torch.equal(ref, got):
