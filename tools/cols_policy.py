@@ -1,8 +1,7 @@
-"""Fused parse + columns vs parse then columns, by requested column bytes per
-frame (the threshold ZP_FUSED_MAX_COL_BYTES of zp_parse_batch_columns_device):
-tools/variants/libzc_fused.so (threshold 1000: always fused) against
-libzc_split.so (threshold 0: always two kernels), interleaved in one process.
-Usage: python tools/cols_policy.py [--configs c3,c5]"""
+"""Fused parse + columns (zp_parse_batch_columns_device) vs parse then columns
+(zp_parse_batch_device + zp_extract_columns_device on the same stream), by
+requested column bytes per frame, interleaved in one process (round 4,
+DESIGN.md §11). Usage: python tools/cols_policy.py [--configs c3,c5]"""
 import argparse
 import ctypes
 import importlib
@@ -38,12 +37,7 @@ def main():
     a = ap.parse_args()
     zp = importlib.import_module("zero-packet_amd")
     C = zp.columns
-    vp, u64 = ctypes.c_void_p, ctypes.c_uint64
-    libs = []
-    for v in ("fused", "split"):
-        l = ctypes.CDLL(os.path.join(ROOT, "tools", "variants", f"libzc_{v}.so"))
-        l.zp_parse_batch_columns_device.argtypes = [vp, vp, vp, u64, vp, vp, vp, vp]
-        libs.append((v, l))
+    lib = zp._lib.hip()
     d = torch.device("cuda:0")
     s = torch.cuda.current_stream(d)
     for cfg in a.configs.split(","):
@@ -58,13 +52,22 @@ def main():
             for k in names:
                 ptrs[C.INDEX[k]] = out[k].data_ptr()
             width = sum(C.width(k) for k in names)
-            res = {v: [] for v, _ in libs}
+            def fused():
+                return lib.zp_parse_batch_columns_device(
+                    arena.data_ptr(), offs.data_ptr(), lens.data_ptr(), n, rec.data_ptr(),
+                    ext.data_ptr(), ptrs, ctypes.c_void_p(s.cuda_stream))
+
+            def split():
+                rc = lib.zp_parse_batch_device(arena.data_ptr(), offs.data_ptr(), lens.data_ptr(),
+                                               n, rec.data_ptr(), ext.data_ptr(),
+                                               ctypes.c_void_p(s.cuda_stream))
+                return rc or lib.zp_extract_columns_device(
+                    arena.data_ptr(), offs.data_ptr(), lens.data_ptr(), rec.data_ptr(), n, ptrs,
+                    ctypes.c_void_p(s.cuda_stream))
+            res = {"fused": [], "split": []}
             ref = None
             for r in range(a.rounds):
-                for v, l in libs:
-                    fn = lambda l=l: l.zp_parse_batch_columns_device(
-                        arena.data_ptr(), offs.data_ptr(), lens.data_ptr(), n, rec.data_ptr(),
-                        ext.data_ptr(), ptrs, s.cuda_stream)
+                for v, fn in (("fused", fused), ("split", split)):
                     assert fn() == 0
                     ev = [(torch.cuda.Event(enable_timing=True),
                            torch.cuda.Event(enable_timing=True)) for _ in range(a.reps)]

@@ -1129,22 +1129,6 @@ extern "C" int zp_parse_batch_device(const uint8_t* arena, const uint64_t* offs,
     return 0;
 }
 
-// Fused or split (round 4): the column stores of the fused
-// kernel go into the parse's read stream, and HBM writes mixed into that
-// stream cost several times their bytes (§4), while the split path re-reads
-// one header window per frame (the column kernel) instead. Past
-// ZP_FUSED_MAX_COL_BYTES requested column bytes per frame the split path is
-// faster (c3, all 29 columns = 73 B: fused +6.7 %; the 5-tuple = 37 B:
-// fused -8.5 %), so the entry point runs the parse kernel and then the column
-// kernel on the stream: the same records and columns either way.
-#ifndef ZP_FUSED_MAX_COL_BYTES
-#define ZP_FUSED_MAX_COL_BYTES 56
-#endif
-extern "C" int zp_col_width(int col);
-extern "C" int zp_extract_columns_device(const uint8_t* arena, const uint64_t* offs,
-                                         const uint32_t* lens, const zp_record* records,
-                                         uint64_t n, void* const* cols, void* stream);
-
 extern "C" int zp_parse_batch_columns_device(const uint8_t* arena, const uint64_t* offs,
                                              const uint32_t* lens, uint64_t n,
                                              zp_record* records, zp_ext_offsets* ext,
@@ -1153,12 +1137,6 @@ extern "C" int zp_parse_batch_columns_device(const uint8_t* arena, const uint64_
     if (!arena || !offs || !lens || !records || !cols) {
         snprintf(g_last_error, sizeof g_last_error, "zp_parse_batch_columns_device: null pointer");
         return -1;
-    }
-    int col_bytes = 0;
-    for (int k = 0; k < ZP_COL_COUNT; ++k) col_bytes += cols[k] ? zp_col_width(k) : 0;
-    if (col_bytes > ZP_FUSED_MAX_COL_BYTES) {
-        const int rc = zp_parse_batch_device(arena, offs, lens, n, records, ext, stream);
-        return rc ? rc : zp_extract_columns_device(arena, offs, lens, records, n, cols, stream);
     }
     ColPtrs c;
     for (int k = 0; k < ZP_COL_COUNT; ++k) c.p[k] = (uint8_t*)cols[k];
