@@ -130,8 +130,20 @@ extern "C" int zp_stamps_set(void* p) {
 // conflict-free for the cooperative ds_write_b128 of phase A and for each
 // lane's ds_read_b128 of its own frame) + global fallback past the window.
 // --------------------------------------------------------------------------
+// ZP_REGION: after the stream each lane copies its frame's window cells out
+// of the swizzled [chunk][rank] layout into a private contiguous LDS region of
+// ZP_RSTRIDE dwords (an odd count: the lanes' reads of one offset fall in 64
+// different banks), so a field read is one ds_read_b32 at region + (y >> 2)
+// instead of a swizzled-cell address (5 VALU) with 4-way bank conflicts.
+#ifndef ZP_REGION
+#define ZP_REGION 1
+#endif
+#define ZP_RSTRIDE (ZP_WIN / 4 + 1)
 struct FrameView {
     const uint4* win;        // this wave's window, [ZP_WIN_CH][64]
+#if ZP_REGION
+    const uint32_t* reg;     // ZP_REGION: this lane's window, ZP_WIN / 4 dwords from A & ~15
+#endif
     const uint8_t* g;        // frame in global memory
     uint32_t lane;
     uint32_t shift;          // frame address & 15 (window starts 16-aligned)
@@ -145,11 +157,19 @@ struct FrameView {
 };
 
 __device__ __forceinline__ uint4 win_chunk(const FrameView& f, uint32_t c) {
+#if ZP_REGION
+    return make_uint4(f.reg[4 * c], f.reg[4 * c + 1], f.reg[4 * c + 2], f.reg[4 * c + 3]);
+#else
     return f.win[c * 64 + (f.lane ^ c)];
+#endif
 }
 __device__ __forceinline__ uint32_t win_dw(const FrameView& f, uint32_t d) {
+#if ZP_REGION
+    return f.reg[d];
+#else
     const uint32_t c = d >> 2;
     return ((const uint32_t*)&f.win[c * 64 + (f.lane ^ c)])[d & 3];
+#endif
 }
 
 // Chunk c (from A & ~15) past the window: one 16-B load per distinct chunk
@@ -879,6 +899,28 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
     fv.wlen = s.wlen;
     fv.xc = make_uint4(0, 0, 0, 0);
     fv.xi = ~0u;
+#if ZP_REGION
+    // the frame's cells and last chunk to registers, then its window to the
+    // lane's private region (it overlays the cells and part of the tails)
+    uint4 mytail;
+    {
+        static_assert(64 * ZP_RSTRIDE * 4 <= (ZP_WIN_CH + 1) * 64 * 16, "regions fit the window LDS");
+        const uint32_t rk = s.rank & 63u;
+        uint4 cell[ZP_WIN_CH];
+#pragma unroll
+        for (uint32_t c = 0; c < ZP_WIN_CH; ++c) cell[c] = lds.win[c * 64 + ((rk ^ c) & 63u)];
+        mytail = tail[rk];
+        wave_lds_fence();
+        uint32_t* reg = (uint32_t*)&lds.win[0] + (uint32_t)lane * ZP_RSTRIDE;
+#pragma unroll
+        for (uint32_t c = 0; c < ZP_WIN_CH; ++c) {
+            reg[4 * c] = cell[c].x; reg[4 * c + 1] = cell[c].y;
+            reg[4 * c + 2] = cell[c].z; reg[4 * c + 3] = cell[c].w;
+        }
+        wave_lds_fence();
+        fv.reg = reg;
+    }
+#endif
     Walk w;
     w.rec = zp_rec_full{};
     w.outer = make_uint4(0, 0, 0, 0);
@@ -931,7 +973,11 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
             const uint32_t r = s.rank;
             const uint32_t fsum = lds.cend[r] - (r ? lds.cend[r - 1] : 0u);
             const uint32_t he = (s.len + s.shift) & 15u;    // bytes of the last chunk in use
+#if ZP_REGION
+            const uint32_t ex = he ? range_sum(mytail, he, 16u) : 0u;
+#else
             const uint32_t ex = he ? range_sum(tail[r], he, 16u) : 0u;
+#endif
 #ifdef ZP_ABL_NO_L4HDR
             ok = csum_ok(w.acc, fsum - ex, odd);                  // timing ablation only
 #else
