@@ -322,3 +322,25 @@ extern "C" int membw_width(const void* p, uint64_t bytes, uint32_t* out, int wid
     else return -1;
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+
+// Write-allocate probe (round 4, the builder's read multiple): a 16-B-chunk
+// copy src -> dst where every 128-B destination line gets only bytes
+// [gap, 128) (gap = 0: whole lines). If FETCH_SIZE grows with gap > 0, partial
+// line writes make the L2 fetch the rest of the line from HBM.
+__global__ void __launch_bounds__(256) copy_gap(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                uint64_t n16, uint32_t gap16) {
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += stride) {
+        if ((uint32_t)(i & 7) < gap16) continue;          // 8 chunks per 128-B line
+        typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 v = __builtin_nontemporal_load((const u32x4*)src + i);
+        ((u32x4*)dst)[i] = v;
+    }
+}
+
+extern "C" int membw_copy_gap(const void* src, void* dst, uint64_t bytes, int gap16, int blocks,
+                              void* stream) {
+    hipLaunchKernelGGL(copy_gap, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                       (const uint4*)src, (uint4*)dst, bytes / 16, (uint32_t)gap16);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}

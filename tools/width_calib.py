@@ -35,6 +35,16 @@ def main():
             torch.cuda.synchronize()
             dt = time.perf_counter() - t
         print(f"width {w}: {nbytes} B per launch, {nbytes / dt / 1e9:.0f} GB/s (wall)", flush=True)
+    # write-allocate probe: copy 2 GiB with 0 / 1 / 4 of every line's 8 chunks left unwritten
+    mb.membw_copy_gap.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int,
+                                  ctypes.c_int, ctypes.c_void_p]
+    half = nbytes // 2
+    for gap in (0, 1, 4):
+        for _ in range(3):
+            assert mb.membw_copy_gap(buf.data_ptr(), buf.data_ptr() + half, half, gap, 8192, s) == 0
+        torch.cuda.synchronize()
+        print(f"copy_gap {gap}: {half} B src, {half * (8 - gap) // 8} B written per launch",
+              flush=True)
 
 
 if __name__ == "__main__":
