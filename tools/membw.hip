@@ -282,7 +282,11 @@ __global__ void __launch_bounds__(256) read_width(const uint8_t* __restrict__ p,
     uint32_t acc = 0;
     const uint64_t stride = (uint64_t)gridDim.x * 256;
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n / W; i += stride) {
-        if constexpr (W == 4) {
+        if constexpr (W == 1) {
+            acc += p[i];
+        } else if constexpr (W == 2) {
+            acc += ((const uint16_t*)p)[i];
+        } else if constexpr (W == 4) {
             acc += __builtin_nontemporal_load((const uint32_t*)p + i);
         } else if constexpr (W == 8) {
             typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
@@ -315,7 +319,9 @@ extern "C" int membw_width(const void* p, uint64_t bytes, uint32_t* out, int wid
                            void* stream) {
     const uint8_t* q = (const uint8_t*)p;
     hipStream_t s = (hipStream_t)stream;
-    if (width == 4) hipLaunchKernelGGL(read_width<4>, dim3(blocks), dim3(256), 0, s, q, bytes, out);
+    if (width == 1) hipLaunchKernelGGL(read_width<1>, dim3(blocks), dim3(256), 0, s, q, bytes, out);
+    else if (width == 2) hipLaunchKernelGGL(read_width<2>, dim3(blocks), dim3(256), 0, s, q, bytes, out);
+    else if (width == 4) hipLaunchKernelGGL(read_width<4>, dim3(blocks), dim3(256), 0, s, q, bytes, out);
     else if (width == 8) hipLaunchKernelGGL(read_width<8>, dim3(blocks), dim3(256), 0, s, q, bytes, out);
     else if (width == 16) hipLaunchKernelGGL(read_width<16>, dim3(blocks), dim3(256), 0, s, q, bytes, out);
     else if (width == 5) hipLaunchKernelGGL(read_stride5, dim3(blocks), dim3(256), 0, s, q, bytes, out);

@@ -27,7 +27,7 @@ def main():
     buf = torch.randint(0, 255, (nbytes,), dtype=torch.uint8, device="cuda")
     out = torch.zeros(1 << 16, dtype=torch.int32, device="cuda")
     s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-    for w in (4, 8, 16, 5):
+    for w in (1, 2, 4, 8, 16, 5):
         for _ in range(3):
             torch.cuda.synchronize()
             t = time.perf_counter()
