@@ -67,6 +67,9 @@
 #ifndef ZP_SMALL_G
 #define ZP_SMALL_G 4         // tiles of at most this many stream items take one small group (0: off)
 #endif
+#ifndef ZP_TAIL_G
+#define ZP_TAIL_G 4          // a tile's last <= this many items as one small group (0: off)
+#endif
 // Timing-only ablations and diagnostics (tools/build_variants.sh,
 // tools/alloc_probe.py --no-check); never set in the product:
 //   ZP_ABL_FAKE_WALK  replace the walk by "pending L4 at offset 42"
@@ -1113,6 +1116,28 @@ __device__ __forceinline__ void parse_tiles(const uint8_t* __restrict__ arena,
         STAMP(2);
         consume_group<ZP_G>(0, s.nitems, lane, va, ka, win, tail, lds.cend, s.run);
         for (uint32_t i0 = ZP_G; i0 < s.nitems; i0 += ZP_G) {
+#if ZP_TAIL_G2
+            if (s.nitems - i0 <= 2) {                 // A/B: the last 1-2 items as a pair
+                uint4 vt[2];
+                uint32_t kt[2];
+                issue_group<2>(i0, s.nitems, s.cur, s.R, lane, fallback, vt, kt);
+                consume_group<2>(i0, s.nitems, lane, vt, kt, win, tail, lds.cend, s.run);
+                break;
+            }
+#endif
+#if ZP_TAIL_G
+            // The last <= ZP_TAIL_G items as a small group: fewer dummy loads
+            // past the tile's end, whose address work (4 ds_bpermute each) and
+            // consume are not free (c5 -1.7 %, c6 -1.1 %, c3 -0.3 %, c4 0;
+            // profiles/r04_kbench_tail_group.log). Wave-uniform.
+            if (s.nitems - i0 <= ZP_TAIL_G) {
+                uint4 vt[ZP_TAIL_G];
+                uint32_t kt[ZP_TAIL_G];
+                issue_group<ZP_TAIL_G>(i0, s.nitems, s.cur, s.R, lane, fallback, vt, kt);
+                consume_group<ZP_TAIL_G>(i0, s.nitems, lane, vt, kt, win, tail, lds.cend, s.run);
+                break;
+            }
+#endif
             issue_group<ZP_G>(i0, s.nitems, s.cur, s.R, lane, fallback, va, ka);
             consume_group<ZP_G>(i0, s.nitems, lane, va, ka, win, tail, lds.cend, s.run);
         }
