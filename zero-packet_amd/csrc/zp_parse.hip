@@ -70,6 +70,9 @@
 #ifndef ZP_TAIL_G
 #define ZP_TAIL_G 4          // a tile's last <= this many items as one small group (0: off)
 #endif
+#ifndef ZP_TAIL_G2
+#define ZP_TAIL_G2 1         // ... and the last <= 2 as a pair (c5 -0.5 %, c6 -0.6 %)
+#endif
 // Timing-only ablations and diagnostics (tools/build_variants.sh,
 // tools/alloc_probe.py --no-check); never set in the product:
 //   ZP_ABL_FAKE_WALK  replace the walk by "pending L4 at offset 42"
@@ -1117,7 +1120,7 @@ __device__ __forceinline__ void parse_tiles(const uint8_t* __restrict__ arena,
         consume_group<ZP_G>(0, s.nitems, lane, va, ka, win, tail, lds.cend, s.run);
         for (uint32_t i0 = ZP_G; i0 < s.nitems; i0 += ZP_G) {
 #if ZP_TAIL_G2
-            if (s.nitems - i0 <= 2) {                 // A/B: the last 1-2 items as a pair
+            if (s.nitems - i0 <= 2) {                 // the last 1-2 items as a pair
                 uint4 vt[2];
                 uint32_t kt[2];
                 issue_group<2>(i0, s.nitems, s.cur, s.R, lane, fallback, vt, kt);
