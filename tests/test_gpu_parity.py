@@ -211,6 +211,40 @@ def test_layouts(zp, golden, layout):
     assert_same(got, gext, want, wext)
 
 
+def test_frames_far_apart_in_one_tile(zp, golden):
+    """Frames of one tile 17 GiB apart: the stream's per-frame 64-bit chunk
+    origins (a tile is not a contiguous region). A 17 GiB arena with the
+    frames of every other tile split between its two ends, alternating
+    within the tile."""
+    frames = fuzz_frames(zp, golden, 512, 29, repair_p=0.5)
+    gap = 17 << 30
+    d = dev()
+    arena = torch.zeros(gap + (1 << 20), dtype=torch.uint8, device=d)
+    lo = hi = 0
+    offs = []
+    for i, f in enumerate(frames):
+        tile_split = (i // 64) % 2 == 1
+        if tile_split and i % 2:
+            offs.append(gap + hi); hi += len(f) + 1
+        else:
+            offs.append(lo); lo += len(f) + 1
+    assert lo < gap and hi < (1 << 20)
+    for o, f in zip(offs, frames):
+        if f:
+            arena[o:o + len(f)] = torch.frombuffer(bytearray(f), dtype=torch.uint8).to(d)
+    offs_t = torch.tensor(offs, dtype=torch.int64, device=d)
+    lens_t = torch.tensor([len(f) for f in frames], dtype=torch.int32, device=d)
+    r, e = zp.batch.parse_batch(arena, offs_t, lens_t)
+    torch.cuda.synchronize()
+    got, gext = zp.batch.records_to_numpy(r, e)
+    del arena
+    torch.cuda.empty_cache()
+    a, o, l_ = pack(frames)
+    want, wext = orc.parse_batch(a, o, l_)
+    assert_same(got, gext, want, wext)
+    assert (want["err"] == 0).sum() > 100
+
+
 def test_edge_lengths_and_empty(zp):
     d = dev()
     # n == 0: no launch, no error
