@@ -751,6 +751,7 @@ struct WinCsum {
     uint4 tail;                       // the frame's last chunk (original bytes)
     uintptr_t ga;
     uint32_t shift, len, nchw, fsum;
+    bool wo;                          // window-only stream (ZB_SKIP_PAY): no bytes past the end
     uint32_t vorig[ZP_WIN_CH];
     // what csum() saw, for a payload copied past the window after the chain
     // (coop_payload): the checksum is then refolded with the copy's V change
@@ -768,7 +769,7 @@ struct WinCsum {
                 else if (c == c4) before += range_sum(q, 0, y4 & 15);
             }
         }
-        const uint32_t he = (len + shift) & 15u;
+        const uint32_t he = wo ? 0u : (len + shift) & 15u;
         const uint32_t ex = he ? range_sum(tail, he, 16u) : 0u;
         const uint32_t V = vall - before - ex;
         cs_V = V; cs_acc = acc; cs_l4 = l4;
@@ -833,6 +834,12 @@ __device__ __forceinline__ uint32_t chain_extent(const Ops& ops, uint32_t nops, 
 #endif
 #ifndef ZB_LANE_PAY
 #define ZB_LANE_PAY 1          // payload copies past the window on the lane path
+#endif
+#ifndef ZB_SKIP_PAY
+#define ZB_SKIP_PAY 1          // payload frames stream their window only (ZB_LANE_PAY, ZB_OP_PREFETCH)
+#endif
+#if ZB_SKIP_PAY && !(ZB_LANE_PAY && ZB_OP_PREFETCH)
+#error "ZB_SKIP_PAY needs ZB_LANE_PAY and ZB_OP_PREFETCH"
 #endif
 #ifndef ZB_WIDE_EDGES
 #define ZB_WIDE_EDGES 1        // partial 16-B chunks by dword/short/byte stores (0: byte loop)
@@ -983,12 +990,14 @@ struct SumChunk { uint4 q; uint32_t l, h, neg; };
 // end in its last chunk (cB, from the kept original chunk: in HBM they are
 // the next frame's, whose lane may be rewriting them).
 __device__ __forceinline__ uint32_t coop_payload(bool go, uintptr_t D0, uintptr_t D1, uintptr_t FE,
-                                                 uintptr_t src, uint32_t cB, int lane) {
+                                                 uintptr_t src, uint32_t cB, int lane,
+                                                 bool wo = false) {
     const uint32_t mc = go ? (uint32_t)(D1 - D0) : 0u;
-    const bool kA = mc <= (uint32_t)(FE - D1);
+    const bool kA = !wo && mc <= (uint32_t)(FE - D1);   // wo frames: kind B (D0..D1 never read)
     const uintptr_t R0 = kA ? D0 : (D1 & ~(uintptr_t)15);
-    const uint32_t rlo = go ? (uint32_t)((kA ? D0 : D1) - R0) : 0u;
-    const uint32_t rhi = go ? (uint32_t)((kA ? D1 : FE) - R0) : 0u;
+    const bool rd = go && (kA || FE > D1);             // (a copy to the frame end reads nothing)
+    const uint32_t rlo = rd ? (uint32_t)((kA ? D0 : D1) - R0) : 0u;
+    const uint32_t rhi = rd ? (uint32_t)((kA ? D1 : FE) - R0) : 0u;
     // pass 1: original bytes (loads only)
     const uint32_t vo = wave_segments<SumChunk>(
         (rhi + 15) >> 4, lane,
@@ -1079,10 +1088,30 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
     const uint32_t pf0 = op_start[ipc], pf1 = op_start[ipc + 1];
     load_desc(arena, offs, lens, n, t, lane, len, ga);
     TileState s;
-    tile_setup(s, t, len, ga, n, lane, lds);
 #if ZB_OP_PREFETCH && ZB_LANE_PAY
     OpHeads oh{OpGlobal{ops + (ip < n ? pf0 : 0u)}};
     oh.load(ip < n && pf1 >= pf0 ? pf1 - pf0 : 0u);
+#endif
+#if ZB_SKIP_PAY
+    // A frame whose final payload copy replaces at least as many bytes past
+    // the window as follow the copy streams its window only (wo): the bytes
+    // the copy replaces are never read, the ones after it are read by the
+    // copy's first pass, and the L4 sum is built from the new window, the
+    // copy and those. Deciding it needs the chain's heads before the stream.
+    bool wo = false;
+    if (ip < n && pf1 >= pf0 && len >= 64 && len <= ZP_GIANT) {
+        uint32_t pa = 0, pl = 0;
+        const uint32_t sh0 = (uint32_t)(ga & 15);
+        const uint32_t wl0 = len < ZP_WIN - sh0 ? len : ZP_WIN - sh0;
+        if (chain_extent(oh, pf1 - pf0, &pa, &pl) <= wl0 && pl && pa + pl > wl0) {
+            const uint32_t pe = pa + pl;
+            wo = pe <= len && pe - wl0 >= len - pe;
+        }
+    }
+    tile_setup(s, t, len, ga, n, lane, lds, wo);
+#else
+    const bool wo = false;
+    tile_setup(s, t, len, ga, n, lane, lds);
 #endif
     uint4 va[ZP_G];
     uint32_t ka[ZP_G];
@@ -1138,6 +1167,7 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
         wc.nchw = nch < ZP_WIN_CH ? nch : ZP_WIN_CH;
         wc.fsum = lds.cend[s.rank] - (s.rank ? lds.cend[s.rank - 1] : 0u);
         wc.tail = tail[rank];
+        wc.wo = wo;
         ptail = tail[(rank - 1) & 63u];
 #pragma unroll
         for (uint32_t c = 0; c < ZP_WIN_CH; ++c) {
@@ -1185,11 +1215,11 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
             uint32_t Vw = 0;
 #pragma unroll
             for (uint32_t c = 0; c < ZP_WIN_CH; ++c) Vw += wc.vorig[c];
-            const uint32_t he = (len + s.shift) & 15u;
-            cB = Vw + (he ? range_sum(wc.tail, he, 16u) : 0u) - wc.fsum;
+            const uint32_t he = wo ? 0u : (len + s.shift) & 15u;
+            cB = Vw + (he ? range_sum(wc.tail, he, 16u) : 0u) - wc.fsum;   // 0 for wo frames
         }
         const uint32_t delta = coop_payload(go, s.ga + s.wlen, s.ga + pe, s.ga + len, src, cB,
-                                            lane);
+                                            lane, wo);
         ZB_STAMP(4);
         if (go) {                                      // refold the L4 checksum
             const uint32_t k4 = og.kind(nops - 1);
@@ -1236,7 +1266,9 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
                          bperm((uint32_t)wend, pl);
     const uint32_t pLen = bperm(s.live ? len : 0u, pl);
     const uintptr_t S0 = s.ga & ~(uintptr_t)63;
-    const bool pre = fast && lane && hwc && (s.ga & 63u) && pLen >= 64 && pLen <= ZP_GIANT &&
+    // (a window-only previous frame has no last chunks in t4 / tail)
+    const bool pwo = bperm(wo ? 1u : 0u, pl) != 0u;
+    const bool pre = fast && lane && hwc && (s.ga & 63u) && pLen >= 64 && pLen <= ZP_GIANT && !pwo &&
                      pA + pLen == s.ga &&
                      S0 >= pA && S0 >= pW;
     if (pre) {

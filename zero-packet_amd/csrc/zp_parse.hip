@@ -81,6 +81,7 @@
 //   ZP_ABL_EXTRA=n    n extra dependent VALU per stream item (zp_stream.h)
 //   ZP_ABL_NO_IPSUM / ZP_ABL_NO_PSEUDO / ZP_ABL_NO_L4HDR  skip one header sum
 //   ZP_ABL_NOREC      no record stores
+//   ZP_ABL_REC4       4-B record stores at 4 * i (wrong contents, timing only)
 //   ZP_STAMPS         per-wave phase timestamps (tools/stamps.py)
 //   ZP_DBG_FBCOUNT    count past-window chunk loads (tools/fbcount.py)
 
@@ -869,7 +870,11 @@ __device__ __forceinline__ bool tiny_tile(uint64_t tile, uint32_t len, uintptr_t
     if (live) {
         // Ethernet II (code 0), IPv4, the L4 reader at 34
         const uint32_t flags = ZP_F_ETHERNET | ZP_F_IPV4 | (tcp ? ZP_F_TCP : udp ? ZP_F_UDP : ZP_F_ICMPV4);
+#ifdef ZP_ABL_REC4
+        __builtin_nontemporal_store(flags ^ 34u, (uint32_t*)records + tile * 64 + lane);
+#else
         __builtin_nontemporal_store(zp_u32x2{flags, 34u}, (zp_u32x2*)(records + tile * 64 + lane));
+#endif
     }
     return true;
 }
@@ -1008,7 +1013,13 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
         // arena and the records: nt took 6-7 % off on every
         // placement, 16-B records (v2) 4-6 % against 32-B ones, and 8-B
         // records (v4) 2-7 % more.
+#ifdef ZP_ABL_REC4
+        // Timing probe only (wrong contents): a 4-B record at byte 4 * p
+        const zp_u32x2 q = zp_pack(rec);
+        __builtin_nontemporal_store(q.x ^ q.y, (uint32_t*)records + p);
+#else
         __builtin_nontemporal_store(zp_pack(rec), (zp_u32x2*)(records + p));
+#endif
     }
     if (ext) {
         // The extension chains: a wave with at least ZP_EXT_DENSE chains

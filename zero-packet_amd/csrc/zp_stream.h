@@ -320,7 +320,8 @@ struct TileState {
 // Chunk ranges, ranks and the compacted per-rank frame table of a tile.
 // len = 0 lanes (past the batch) own no chunks.
 __device__ __forceinline__ void tile_setup(TileState& s, uint64_t tile, uint32_t len,
-                                           uintptr_t ga, uint64_t n, int lane, WaveLds& lds) {
+                                           uintptr_t ga, uint64_t n, int lane, WaveLds& lds,
+                                           bool win_only = false) {
     s.tile = tile;
     s.ga = ga;
     s.len = len;
@@ -330,7 +331,9 @@ __device__ __forceinline__ void tile_setup(TileState& s, uint64_t tile, uint32_t
     s.shift = (uint32_t)(ga & 15);
     s.wlen = len < ZP_WIN - s.shift ? len : ZP_WIN - s.shift;
     s.giant = len > ZP_GIANT;
-    const uint32_t span = s.giant ? (uint32_t)ZP_WIN : len + s.shift;
+    // win_only (the builder's payload frames): the window only, like giants
+    const uint32_t span = s.giant || (win_only && len + s.shift > ZP_WIN) ? (uint32_t)ZP_WIN
+                                                                          : len + s.shift;
     const uint32_t nch = len >= 64 ? (span + 15) >> 4 : 0u;
     const uint64_t M = __ballot(nch > 0);
     s.rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(M >> 32),
