@@ -26,6 +26,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=1 << 22)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--rounds", type=int, default=1,
+                    help="interleaved timing rounds over the libs (median of the round medians)")
     ap.add_argument("--variants", default="", help="tools/variants/libzb_<name>.so builds to A/B")
     ap.add_argument("--payload", type=int, default=0,
                     help="copy min(P, room) payload bytes from the data blob into each frame "
@@ -156,13 +158,16 @@ def main():
     blob_read = int(pay.sum()) if args.payload and not args.shared_blob else 0
     errs = 0
     ref = None
-    for name, lib in libs:
+    def launcher(lib):
         def launch():
             zp._lib.check(lib.zp_build_batch_device(arena.data_ptr(), offs.data_ptr(),
                                                     lens.data_ptr(), n, t_ops.data_ptr(),
                                                     t_start.data_ptr(), t_data.data_ptr(),
                                                     res.data_ptr(), s.cuda_stream),
                           "zp_build_batch_device")
+        return launch
+    for name, lib in libs:
+        launch = launcher(lib)
         arena.copy_(snapshot)
         launch()
         torch.cuda.synchronize()
@@ -171,12 +176,19 @@ def main():
         elif not torch.equal(ref, arena):
             print(f"  !! {name}: built bytes differ from base", flush=True)
         errs += int((res[:, 4] != 0).sum())
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-              for _ in range(args.reps)]
-        for a, b in ev:
-            a.record(s); launch(); b.record(s)
-        torch.cuda.synchronize()
-        ms = float(np.median([a.elapsed_time(b) for a, b in ev]))
+    times = {name: [] for name, _ in libs}
+    for _ in range(args.rounds):
+        for name, lib in libs:
+            launch = launcher(lib)
+            launch()
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                  for _ in range(args.reps)]
+            for a, b in ev:
+                a.record(s); launch(); b.record(s)
+            torch.cuda.synchronize()
+            times[name].append(float(np.median([a.elapsed_time(b) for a, b in ev])))
+    for name, _ in libs:
+        ms = float(np.median(times[name]))
         nbytes = int(ln.sum())
         hdr = exact_write
         opb = int(t_ops.numel() + t_start.numel() * 4)

@@ -841,6 +841,13 @@ __device__ __forceinline__ uint32_t chain_extent(const Ops& ops, uint32_t nops, 
 #if ZB_SKIP_PAY && !(ZB_LANE_PAY && ZB_OP_PREFETCH)
 #error "ZB_SKIP_PAY needs ZB_LANE_PAY and ZB_OP_PREFETCH"
 #endif
+#ifndef ZB_COPY_X4
+#define ZB_COPY_X4 1           // payload copy: one dwordx4 per whole chunk + the next lane's dword
+                               // (instead of 5 dword loads: P = 1000 -3.0 %, r04_build_copy_ab.log)
+#endif
+#ifndef ZB_NT_COPY
+#define ZB_NT_COPY 0           // nontemporal blob loads and whole-chunk stores in the payload copy
+#endif
 #ifndef ZB_WIDE_EDGES
 #define ZB_WIDE_EDGES 1        // partial 16-B chunks by dword/short/byte stores (0: byte loop)
 #endif
@@ -871,7 +878,7 @@ extern "C" int zb_stamps_set(void* p) {
 // wrapping sum of its own chunks' contributions (running-sum differences:
 // no segmented reduction). Every lane must be active (DPP scans, bpermute).
 #ifndef ZB_COOP_U
-#define ZB_COOP_U 4            // without ZB_PIPE_SEARCH 1: 2.04 / 3.52 ms, 2: 1.95 / 3.16, 4: 1.99 / 3.26, 8: 2.11 / 3.52 (P = 200 / 1000); with it 2: 1.85 / 2.80, 4: 1.82 / 2.71, 8: 1.82 / 2.70
+#define ZB_COOP_U 8            // round 4, with ZB_SKIP_PAY and ZB_COPY_X4: 8 vs 4 P = 1000 -1.1 %, P = 200 -0.2 %; round 3, without ZB_PIPE_SEARCH 1: 2.04 / 3.52 ms, 2: 1.95 / 3.16, 4: 1.99 / 3.26, 8: 2.11 / 3.52 (P = 200 / 1000); with it 2: 1.85 / 2.80, 4: 1.82 / 2.71, 8: 1.82 / 2.70
 #endif
 // ZB_PIPE_SEARCH: the owner search of the next ZB_COOP_U items (dependent
 // ds_bpermute round trips) is issued while this round's loads are in flight,
@@ -973,7 +980,7 @@ __device__ __forceinline__ void store_bytes(uintptr_t X, uint4 q, uint32_t s, ui
     if (b < e) *(ZP_GLOBAL uint8_t*)(X + b) = (uint8_t)(q_dw(q, b >> 2) >> (8 * (b & 3u)));
 }
 
-struct CopyChunk { uint32_t x[5]; uintptr_t X; uint32_t m, sh; };
+struct CopyChunk { uint32_t x[5]; uintptr_t X; uint32_t m, sh; bool nb; };
 struct SumChunk { uint4 q; uint32_t l, h, neg; };
 
 // The payload bytes past the window, for every lane whose chain copied a
@@ -1029,21 +1036,57 @@ __device__ __forceinline__ uint32_t coop_payload(bool go, uintptr_t D0, uintptr_
             const uintptr_t S = s0 + 16u * k, sb = S & ~(uintptr_t)3, send = S + c.m;
             c.sh = (uint32_t)(S & 3);
             c.X = d0 + 16u * k;
+#if ZB_COPY_X4
+            // Whole chunks: one dwordx4 from the dword below S; the 5th dword
+            // is the next lane's first when it holds this copy's next chunk
+            // (nb), else its own dword load. A copy's last chunk: dword loads
+            // that stop at its end (no read past the blob range).
+            const bool full = c.m == 16;
+            const uint32_t jn = bperm(j, (uint32_t)lane + 1u), kn = bperm(k, (uint32_t)lane + 1u);
+            const bool ln = bperm(live ? 1u : 0u, (uint32_t)lane + 1u) != 0u;
+            c.nb = lane < 63 && ln && jn == j && kn == k + 1u;
+            if (live && full) {
+                const zp_u32x4 v = *(const ZP_GLOBAL zp_u32x4*)sb;
+                c.x[0] = v.x; c.x[1] = v.y; c.x[2] = v.z; c.x[3] = v.w;
+                c.x[4] = c.sh && !c.nb ? *(const ZP_GLOBAL uint32_t*)(sb + 16u) : 0u;
+            } else {
+#pragma unroll
+                for (int u = 0; u < 5; ++u) {
+                    const uintptr_t a = sb + 4u * u;
+                    c.x[u] = live && a < send ? *(const ZP_GLOBAL uint32_t*)a : 0u;
+                }
+            }
+#else
 #pragma unroll
             for (int u = 0; u < 5; ++u) {
                 const uintptr_t a = sb + 4u * u;
+#if ZB_NT_COPY
+                c.x[u] = live && a < send ? __builtin_nontemporal_load((const ZP_GLOBAL uint32_t*)a) : 0u;
+#else
                 c.x[u] = live && a < send ? *(const ZP_GLOBAL uint32_t*)a : 0u;
+#endif
             }
+#endif
             return c;
         },
         [&](const CopyChunk& c, uint32_t, uint32_t, bool live) {
+#if ZB_COPY_X4
+            const uint32_t x1 = bperm(c.x[0], (uint32_t)lane + 1u);   // every lane (bpermute)
+            const uint32_t x4 = c.m == 16 && c.nb ? x1 : c.x[4];
+#else
+            const uint32_t x4 = c.x[4];
+#endif
             if (!live) return 0u;
             const uint4 q = make_uint4(__builtin_amdgcn_alignbyte(c.x[1], c.x[0], c.sh),
                                        __builtin_amdgcn_alignbyte(c.x[2], c.x[1], c.sh),
                                        __builtin_amdgcn_alignbyte(c.x[3], c.x[2], c.sh),
-                                       __builtin_amdgcn_alignbyte(c.x[4], c.x[3], c.sh));
+                                       __builtin_amdgcn_alignbyte(x4, c.x[3], c.sh));
             if (c.m == 16) {
+#if ZB_NT_COPY
+                __builtin_nontemporal_store(zp_u32x4{q.x, q.y, q.z, q.w}, (ZP_GLOBAL zp_u32x4*)c.X);
+#else
                 *(ZP_GLOBAL zp_u32x4*)c.X = zp_u32x4{q.x, q.y, q.z, q.w};
+#endif
             } else {
 #if ZB_WIDE_EDGES
                 store_bytes(c.X, q, 0, c.m);
