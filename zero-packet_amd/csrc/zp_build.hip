@@ -172,6 +172,11 @@ __device__ __forceinline__ void wave_sync() {
 // LDS layout (the lane-per-frame path, zp_build_fast_kernel).
 enum { ZB_M_COOP = 0, ZB_M_GLOBAL = 1, ZB_M_WIN = 2 };
 
+#ifndef ZB_WIN_COPY_DW
+#define ZB_WIN_COPY_DW 0       // 1: ZB_M_WIN blob copies by dword loads (chain phase -22 %, kernel
+                               // P = 1000 0, P = 200 +2.3 %: r04_build_wincopy_ab.log)
+#endif
+
 // Copies `len` bytes of the data blob to frame offset `at`.
 template <int MODE, typename P>
 __device__ void bcopy(BView<P>& v, uint32_t at, const uint8_t* src, uint32_t len, int lane) {
@@ -208,7 +213,46 @@ __device__ void bcopy(BView<P>& v, uint32_t at, const uint8_t* src, uint32_t len
         // the part inside the lane's window; a payload past it goes to HBM
         // after the chain (zp_build_fast_kernel)
         const uint32_t m = at >= v.lim ? 0u : (v.lim - at < len ? v.lim - at : len);
+#if ZB_WIN_COPY_DW
+        // Dword-aligned blob loads (address space 1, 9 in flight), realigned
+        // to the destination's dwords with alignbyte: whole dwords by one LDS
+        // store, the edges byte by byte. Loads touch only dwords holding
+        // bytes of [src, src + m).
+        if (!m) return;
+        uint8_t ZB_LDSP* dst = (uint8_t ZB_LDSP*)(v.b + at);
+        const uint32_t dmis = (uint32_t)(size_t)dst & 3u;
+        uint32_t ZB_LDSP* dw = (uint32_t ZB_LDSP*)(dst - dmis);
+        const uintptr_t lo = (uintptr_t)src, hi = lo + m;
+        const uintptr_t S0 = lo - dmis;                  // source of dst dword 0's first byte
+        const uint32_t sh = (uint32_t)(S0 & 3u);
+        const uintptr_t g0 = S0 & ~(uintptr_t)3;
+        const uint32_t nw = (dmis + m + 3) >> 2;
+        for (uint32_t w0 = 0; w0 < nw; w0 += 8) {
+            uint32_t x[9];
+#pragma unroll
+            for (uint32_t u = 0; u < 9; ++u) {
+                const uintptr_t a = g0 + 4u * (w0 + u);
+                x[u] = w0 + u <= nw && a + 4u > lo && a < hi ? *(const ZP_GLOBAL uint32_t*)a : 0u;
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < 8; ++u) {
+                const uint32_t w = w0 + u;
+                if (w < nw) {
+                    const uint32_t val = __builtin_amdgcn_alignbyte(x[u + 1], x[u], sh);
+                    const int p0 = (int)(4u * w) - (int)dmis;
+                    if (p0 >= 0 && p0 + 4 <= (int)m) {
+                        dw[w] = val;
+                    } else {
+#pragma unroll
+                        for (int b = 0; b < 4; ++b)
+                            if (p0 + b >= 0 && p0 + b < (int)m) dst[p0 + b] = (uint8_t)(val >> (8 * b));
+                    }
+                }
+            }
+        }
+#else
         for (uint32_t q = 0; q < m; ++q) v.b[at + q] = src[q];
+#endif
     } else {
         for (uint32_t q = 0; q < len; ++q) v.b[at + q] = src[q];
     }
@@ -306,7 +350,7 @@ struct NoWin {
 #define ZB_OP_NEXT 0
 #endif
 template <int MODE, typename P, typename OPS, typename WC>
-__device__ int run_chain(BView<P>& v, const uint8_t ZB_LDSP* stage, uint32_t shift,
+__device__ __forceinline__ int run_chain(BView<P>& v, const uint8_t ZB_LDSP* stage, uint32_t shift,
                          const OPS& ops, uint32_t nops, const WC& wc,
                          const uint8_t* __restrict__ data, int lane, uint32_t* hl_out,
                          uint32_t* done_out, uint32_t* hw_out) {
