@@ -26,6 +26,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=1 << 22)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--no-base", action="store_true",
+                    help="time only the first of --variants (PMC passes of a variant)")
     ap.add_argument("--rounds", type=int, default=1,
                     help="interleaved timing rounds over the libs (median of the round medians)")
     ap.add_argument("--variants", default="", help="tools/variants/libzb_<name>.so builds to A/B")
@@ -110,6 +112,8 @@ def main():
         l_.zp_build_batch_device.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_uint64] + \
             [ctypes.c_void_p] * 5
         libs.append((v, l_))
+    if args.no_base:
+        libs = libs[1:2]
     # The write floor at HBM granularity: every frame's written range
     # [A, A + headers + payload) rounded out to whole 64-B sectors (the
     # granularity of WRITE_SIZE / TCC_EA0_WRREQ), sectors shared by

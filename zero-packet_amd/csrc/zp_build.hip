@@ -212,7 +212,11 @@ __device__ void bcopy(BView<P>& v, uint32_t at, const uint8_t* src, uint32_t len
     } else if constexpr (MODE == ZB_M_WIN) {
         // the part inside the lane's window; a payload past it goes to HBM
         // after the chain (zp_build_fast_kernel)
+#ifdef ZB_ABL_NOWINCOPY
+        const uint32_t m = 0;                        // timing probe only: no window part
+#else
         const uint32_t m = at >= v.lim ? 0u : (v.lim - at < len ? v.lim - at : len);
+#endif
 #if ZB_WIN_COPY_DW
         // Dword-aligned blob loads (address space 1, 9 in flight), realigned
         // to the destination's dwords with alignbyte: whole dwords by one LDS
@@ -353,7 +357,8 @@ template <int MODE, typename P, typename OPS, typename WC>
 __device__ __forceinline__ int run_chain(BView<P>& v, const uint8_t ZB_LDSP* stage, uint32_t shift,
                          const OPS& ops, uint32_t nops, const WC& wc,
                          const uint8_t* __restrict__ data, int lane, uint32_t* hl_out,
-                         uint32_t* done_out, uint32_t* hw_out) {
+                         uint32_t* done_out, uint32_t* hw_out, uint32_t* doff_out = nullptr,
+                         uint32_t* kind_out = nullptr) {
     int st = BS_RAW;
     *hw_out = 0;
     for (uint32_t k = 0; k < nops; ++k) {            // typestate (compile time in Rust)
@@ -379,6 +384,8 @@ __device__ __forceinline__ int run_chain(BView<P>& v, const uint8_t ZB_LDSP* sta
         const bool has = o.data_len != ZP_BUILD_NO_DATA;
         const uint32_t dl = has ? o.data_len : 0u;
         const uint8_t* d = data + o.data_off;
+        if (doff_out) *doff_out = o.data_off;        // the last op's, for the copy past the window
+        if (kind_out) *kind_out = o.kind;
         const uint32_t sl = n - hl;                  // &mut bytes[header_len..]
         const uint32_t base = hl;
         P s = v.b + hl;
@@ -733,6 +740,62 @@ struct OpGlobal {
 #ifndef ZB_OPH
 #define ZB_OPH 4
 #endif
+#ifndef ZB_OP_FULL
+#define ZB_OP_FULL 0           // 1: the first 3 ops whole in registers from before the stream
+#endif
+#if ZB_OP_FULL
+// The first 3 ops whole, loaded once before the stream (each op line is read
+// once; with heads only, the ops are read again after the stream). Three
+// named ops, selected with ternaries: an array indexed by k goes to scratch.
+struct OpQ { zp_u32x4 a, b, c, d; };
+struct OpHeads {
+    OpGlobal og;
+    OpQ f0, f1, f2;
+    __device__ __forceinline__ static OpQ ld(const zp_build_op* g, bool on) {
+        const ZP_GLOBAL zp_u32x4* q = (const ZP_GLOBAL zp_u32x4*)g;
+        const zp_u32x4 z{0, 0, 0, 0};
+        OpQ o;
+        o.a = on ? q[0] : z; o.b = on ? q[1] : z; o.c = on ? q[2] : z; o.d = on ? q[3] : z;
+        return o;
+    }
+    __device__ __forceinline__ void load(uint32_t nops) {
+        f0 = ld(og.g, nops > 0);
+        f1 = ld(og.g + (nops > 1 ? 1 : 0), nops > 1);
+        f2 = ld(og.g + (nops > 2 ? 2 : 0), nops > 2);
+    }
+    // (the values pass an empty asm first: a select of loads from one
+    // aggregate would otherwise become one load at a computed address, and
+    // the aggregate would live in scratch)
+    __device__ __forceinline__ static zp_u32x4 pick(uint32_t k, zp_u32x4 x, zp_u32x4 y, zp_u32x4 z) {
+        asm volatile("" : "+v"(x), "+v"(y), "+v"(z));
+        return k == 0 ? x : k == 1 ? y : z;
+    }
+    __device__ __forceinline__ OpQ sel(uint32_t k) const {
+        OpQ o;
+        o.a = pick(k, f0.a, f1.a, f2.a);
+        o.b = pick(k, f0.b, f1.b, f2.b);
+        o.c = pick(k, f0.c, f1.c, f2.c);
+        o.d = pick(k, f0.d, f1.d, f2.d);
+        return o;
+    }
+    __device__ __forceinline__ uint2 head(uint32_t k) const {
+        if (k >= 3) return og.head(k);
+        const OpQ o = sel(k);
+        return make_uint2(o.a.x, o.b.w);
+    }
+    __device__ __forceinline__ zp_build_op get(uint32_t k) const {
+        OpQ q = sel(k);
+        if (k >= 3) q = ld(og.g + k, true);
+        const zp_u32x4 t[4] = {q.a, q.b, q.c, q.d};
+        zp_build_op o;
+        __builtin_memcpy(&o, t, sizeof o);
+        return o;
+    }
+    __device__ __forceinline__ uint32_t kind(uint32_t k) const {
+        return k < 3 ? (head(k).x & 0xFFu) : og.kind(k);
+    }
+};
+#else
 struct OpHeads {
     OpGlobal og;
     uint2 h[ZB_OPH];
@@ -752,6 +815,7 @@ struct OpHeads {
         return k < ZB_OPH ? (head(k).x & 0xFFu) : og.kind(k);
     }
 };
+#endif
 #ifndef ZB_OP_KINDS
 #define ZB_OP_KINDS 1          // run_chain's typestate pass reads the prefetched kinds
 #endif
@@ -874,7 +938,7 @@ __device__ __forceinline__ uint32_t chain_extent(const Ops& ops, uint32_t nops, 
 }
 
 #ifndef ZB_FAST_WPE
-#define ZB_FAST_WPE 1
+#define ZB_FAST_WPE 3          // at least 3 waves per SIMD (168 VGPRs): the LDS allows 3
 #endif
 #ifndef ZB_LANE_PAY
 #define ZB_LANE_PAY 1          // payload copies past the window on the lane path
@@ -1145,7 +1209,12 @@ __device__ __forceinline__ uint32_t coop_payload(bool go, uintptr_t D0, uintptr_
     return vn + (go && !kA ? cB + vo : vo);
 }
 
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZB_FAST_WPE)))
+#ifdef ZB_FAST_WPE_MAX
+#define ZB_FAST_WPE_ATTR amdgpu_waves_per_eu(ZB_FAST_WPE, ZB_FAST_WPE_MAX)
+#else
+#define ZB_FAST_WPE_ATTR amdgpu_waves_per_eu(ZB_FAST_WPE)
+#endif
+__global__ void __launch_bounds__(64) __attribute__((ZB_FAST_WPE_ATTR))
 zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs,
                      const uint32_t* __restrict__ lens, uint64_t n,
                      const zp_build_op* __restrict__ ops, const uint32_t* __restrict__ op_start,
@@ -1154,7 +1223,7 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
 #ifndef ZB_NO_SECTOR_WB
     // the 3 chunks before each frame's last one (the previous frame's bytes
     // in a frame's first 64-B sector)
-    __shared__ uint4 t4[64 * 3];
+    __shared__ uint4 t4[64 * ZP_T4N];
     constexpr bool T4 = true;
 #else
     uint4* t4 = nullptr;
@@ -1264,7 +1333,7 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
     }
     wave_lds_fence();                                  // every lane holds its cells
     uint8_t ZB_LDSP* region = (uint8_t ZB_LDSP*)win + lane * ZB_RSTRIDE;
-    uint32_t hl = 0, done = 0, hw = 0;
+    uint32_t hl = 0, done = 0, hw = 0, doff = 0, lkind = 0;
     int err = 0;
     if (fast) {
 #pragma unroll
@@ -1285,7 +1354,7 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
 #else
         err = run_chain<ZB_M_WIN>(v, (const uint8_t ZB_LDSP*)nullptr, s.shift, og, nops, wc,
 #endif
-                                  data, lane, &hl, &done, &hw);
+                                  data, lane, &hl, &done, &hw, &doff, &lkind);
     }
     ZB_STAMP(2);
 #if ZB_LANE_PAY
@@ -1298,7 +1367,7 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
         uintptr_t src = 0;
         uint32_t cB = 0;
         if (go) {
-            src = (uintptr_t)data + og.get(nops - 1).data_off + (s.wlen - pay_at);
+            src = (uintptr_t)data + doff + (s.wlen - pay_at);   // (the chain's last op)
             uint32_t Vw = 0;
 #pragma unroll
             for (uint32_t c = 0; c < ZP_WIN_CH; ++c) Vw += wc.vorig[c];
@@ -1309,7 +1378,7 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
                                             lane, wo);
         ZB_STAMP(4);
         if (go) {                                      // refold the L4 checksum
-            const uint32_t k4 = og.kind(nops - 1);
+            const uint32_t k4 = lkind;                  // the chain's last op (go: all ran)
             const uint32_t at = k4 == ZP_B_TCP ? 16u : k4 == ZP_B_UDP ? 6u : 2u;
             const uint16_t c = fold_v(wc.cs_V + delta, wc.cs_acc, !((s.ga + wc.cs_l4) & 1));
             region[s.shift + wc.cs_l4 + at] = (uint8_t)(c >> 8);
@@ -1357,12 +1426,13 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
     const bool pwo = bperm(wo ? 1u : 0u, pl) != 0u;
     const bool pre = fast && lane && hwc && (s.ga & 63u) && pLen >= 64 && pLen <= ZP_GIANT && !pwo &&
                      pA + pLen == s.ga &&
+                     ((((s.ga - 1) & ~(uintptr_t)15) - S0) >> 4) <= (uintptr_t)ZP_T4N &&
                      S0 >= pA && S0 >= pW;
     if (pre) {
         const uintptr_t lastc = (s.ga - 1) & ~(uintptr_t)15;      // the previous frame's last chunk
         for (uintptr_t X = S0; X < a0; X += 16) {
             const uint32_t d = (uint32_t)((lastc - X) >> 4);      // 0..3
-            const uint4 q = d == 0 ? ptail : t4[(rank - 1) * 3 + d - 1];
+            const uint4 q = d == 0 ? ptail : t4[(rank - 1) * ZP_T4N + d - 1];
             *(ZP_GLOBAL zp_u32x4*)X = zp_u32x4{q.x, q.y, q.z, q.w};
         }
     }

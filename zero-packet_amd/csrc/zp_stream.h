@@ -150,7 +150,10 @@ struct Ranked {          // lane r = frame of rank r
 #define KEEP_IN (1u << 31)     // chunk belongs to a frame (else past the end)
 #define KEEP_WIN (1u << 30)    // chunk index < ZP_WIN_CH: window cell in bits 0-9
 #define KEEP_TAIL (1u << 29)   // frame's last chunk
-#define KEEP_T4 (1u << 28)     // one of the 3 chunks before the frame's last (T4 streams) ...
+#ifndef ZP_T4N
+#define ZP_T4N 3               // chunks kept before each frame's last one (T4 streams, <= 3)
+#endif
+#define KEEP_T4 (1u << 28)     // one of the ZP_T4N chunks before the frame's last (T4 streams) ...
 #define KEEP_T4D(k) (((k) >> 22) & 3u)   // ... at this distance from the last, minus 1
 #define KEEP_CELL(k) ((k) & 0x3FFu)
 #define KEEP_RANK(k) (((k) >> 16) & 63u)
@@ -233,7 +236,7 @@ __device__ __forceinline__ void issue_group(uint32_t i0, uint32_t nitems, Cursor
         uint32_t k = (r & 63u) << 16;
         k |= ci < ZP_WIN_CH ? KEEP_WIN | (ci * 64u + ((r ^ ci) & 63u)) : 0u;
         k |= vv == lv ? KEEP_TAIL : 0u;
-        if (T4) k |= lv - vv - 1u < 3u ? KEEP_T4 | ((lv - vv - 1u) << 22) : 0u;
+        if (T4) k |= lv - vv - 1u < (uint32_t)ZP_T4N ? KEEP_T4 | ((lv - vv - 1u) << 22) : 0u;
         keep[q] = (i < nitems && vv <= lv) ? k | KEEP_IN : 0u;
         const uint32_t vc = vv < lv ? vv : lv;
         a[q] = nitems ? (((uintptr_t)ohi << 32) | olo) + 16ull * vc : fallback;
@@ -271,7 +274,7 @@ __device__ __forceinline__ void consume_group(uint32_t i0, uint32_t nitems, int 
         if (k & KEEP_WIN) win[KEEP_CELL(k)] = v[q];
         // T4 streams (the builder) also keep the 3 chunks before each
         // frame's last one: t4[rank * 3 + distance from the last - 1]
-        if (T4 && (k & KEEP_T4)) t4[KEEP_RANK(k) * 3 + KEEP_T4D(k)] = v[q];
+        if (T4 && (k & KEEP_T4)) t4[KEEP_RANK(k) * ZP_T4N + KEEP_T4D(k)] = v[q];
         uint32_t part = sad16(v[q].x, 0u);
         part = sad16(v[q].y, part);
         part = sad16(v[q].z, part);
