@@ -179,7 +179,8 @@ enum { ZB_M_COOP = 0, ZB_M_GLOBAL = 1, ZB_M_WIN = 2 };
 
 // Copies `len` bytes of the data blob to frame offset `at`.
 template <int MODE, typename P>
-__device__ void bcopy(BView<P>& v, uint32_t at, const uint8_t* src, uint32_t len, int lane) {
+__device__ void bcopy(BView<P>& v, uint32_t at, const uint8_t* src, uint32_t len, int lane,
+                      bool payload = false) {
     if constexpr (MODE == ZB_M_COOP) {
         // Aligned dword loads of the blob (address space 1: they cannot alias
         // the LDS stores, so four are in flight per lane), byte stores to the
@@ -215,7 +216,10 @@ __device__ void bcopy(BView<P>& v, uint32_t at, const uint8_t* src, uint32_t len
 #ifdef ZB_ABL_NOWINCOPY
         const uint32_t m = 0;                        // timing probe only: no window part
 #else
-        const uint32_t m = at >= v.lim ? 0u : (v.lim - at < len ? v.lim - at : len);
+        // (only the final payload copy is cut: extension data lies inside
+        // the chain's extent, which the window holds)
+        const uint32_t lim = payload ? v.lim : ~0u;
+        const uint32_t m = at >= lim ? 0u : (lim - at < len ? lim - at : len);
 #endif
 #if ZB_WIN_COPY_DW
         // Dword-aligned blob loads (address space 1, 9 in flight), realigned
@@ -551,7 +555,7 @@ __device__ __forceinline__ int run_chain(BView<P>& v, const uint8_t ZB_LDSP* sta
                     break;
                 }
                 ext = start + dl > ext ? start + dl : ext;
-                bcopy<MODE>(v, hl + start, d, dl, lane);
+                bcopy<MODE>(v, hl + start, d, dl, lane, true);
             }
             const uint32_t proto = o.kind == ZP_B_TCP ? 6u : o.kind == ZP_B_UDP ? 17u : 58u;
             const uint32_t acc = o.kind == ZP_B_ICMPV4 ? 0u : pseudo(o, v4, proto, sl);
@@ -890,11 +894,12 @@ struct WinCsum {
 // itself wrote: ihl, data offset, extension lengths).
 template <class Ops>
 __device__ __forceinline__ uint32_t chain_extent(const Ops& ops, uint32_t nops, uint32_t* pay_at = nullptr,
-                             uint32_t* pay_len = nullptr) {
+                             uint32_t* pay_len = nullptr, bool* pay_ovl = nullptr) {
     // With pay_at: the final L4 op's payload copy is left out of the extent
     // and reported as [*pay_at, *pay_at + *pay_len) (frame offsets).
     uint32_t hl = 0, top = 0;
     if (pay_at) { *pay_at = 0; *pay_len = 0; }
+    if (pay_ovl) *pay_ovl = false;
     for (uint32_t k = 0; k < nops; ++k) {
         const uint2 hd = ops.head(k);
         struct { uint32_t kind; uint8_t b[2]; uint32_t data_len; } o;
@@ -922,6 +927,7 @@ __device__ __forceinline__ uint32_t chain_extent(const Ops& ops, uint32_t nops, 
             ext = st + dl > 20 ? st + dl : 20; adv = st;
             if (pay_at && k + 1 == nops && dl) {
                 *pay_at = hl + st; *pay_len = dl; ext = st > 20 ? st : 20;
+                if (pay_ovl) *pay_ovl = st < 20;         // (the payload overwrites header fields)
             }
             break;
         }
@@ -949,12 +955,8 @@ __device__ __forceinline__ uint32_t chain_extent(const Ops& ops, uint32_t nops, 
 #if ZB_SKIP_PAY && !(ZB_LANE_PAY && ZB_OP_PREFETCH)
 #error "ZB_SKIP_PAY needs ZB_LANE_PAY and ZB_OP_PREFETCH"
 #endif
-#ifndef ZB_COPY_X4
-#define ZB_COPY_X4 1           // payload copy: one dwordx4 per whole chunk + the next lane's dword
-                               // (instead of 5 dword loads: P = 1000 -3.0 %, r04_build_copy_ab.log)
-#endif
-#ifndef ZB_NT_COPY
-#define ZB_NT_COPY 0           // nontemporal blob loads and whole-chunk stores in the payload copy
+#ifndef ZB_PAY_HDR
+#define ZB_PAY_HDR 1           // the wave copy moves the whole payload (the chain copies none of it)
 #endif
 #ifndef ZB_WIDE_EDGES
 #define ZB_WIDE_EDGES 1        // partial 16-B chunks by dword/short/byte stores (0: byte loop)
@@ -1088,30 +1090,37 @@ __device__ __forceinline__ void store_bytes(uintptr_t X, uint4 q, uint32_t s, ui
     if (b < e) *(ZP_GLOBAL uint8_t*)(X + b) = (uint8_t)(q_dw(q, b >> 2) >> (8 * (b & 3u)));
 }
 
-struct CopyChunk { uint32_t x[5]; uintptr_t X; uint32_t m, sh; bool nb; };
+// f packs the chunk's byte range [lo, m) (bits 0-4, 5-9), the source's
+// offset in its dword (10-11) and nb (12): 8 chunks in flight per lane
+struct CopyChunk { uint32_t x[5]; uintptr_t X; uint32_t f; };
 struct SumChunk { uint4 q; uint32_t l, h, neg; };
 
-// The payload bytes past the window, for every lane whose chain copied a
-// payload that reaches past it (go): destination [D0, D1) of its frame
-// (D0 = the window end, 16-B aligned), from the blob at src. The whole wave
-// moves 16-B chunks: coalesced loads of the blob, full 16-B stores (the last
-// chunk of a copy byte by byte), each blob and frame byte touched once.
-// Returns the copy's change of the frame's V (arena parity): V of the copied
-// bytes at their destination minus V of the bytes they replace. The latter
-// is summed over the shorter of two ranges of original bytes, read before
-// any copy is written (a first pass): [D0, D1) itself (kind A), or the
-// frame's bytes after the copy [D1, FE) (kind B), then V(D0, D1) = the
-// frame's stream sum - its window chunks - V(D1, FE) - the bytes past its
-// end in its last chunk (cB, from the kept original chunk: in HBM they are
-// the next frame's, whose lane may be rewriting them).
-__device__ __forceinline__ uint32_t coop_payload(bool go, uintptr_t D0, uintptr_t D1, uintptr_t FE,
-                                                 uintptr_t src, uint32_t cB, int lane,
-                                                 bool wo = false) {
-    const uint32_t mc = go ? (uint32_t)(D1 - D0) : 0u;
-    const bool kA = !wo && mc <= (uint32_t)(FE - D1);   // wo frames: kind B (D0..D1 never read)
-    const uintptr_t R0 = kA ? D0 : (D1 & ~(uintptr_t)15);
+// The payload bytes past the header, for every lane whose chain ends in a
+// payload copy that reaches past its window (go): destination [D0, D1) of
+// its frame from the blob at src (the payload's first byte). The whole wave
+// moves 16-B chunks of [D0 & ~15, D1): coalesced loads of the blob, full
+// 16-B stores, partial ones by store_bytes. With ZB_PAY_HDR the copy starts
+// at the payload start D0 (the chain copies nothing) and the first chunk,
+// when D0 is not 16-B aligned, is left to the caller (it also holds header
+// bytes, among them the checksum refolded after this pass); without it D0 is
+// the window end W (16-B aligned) and the chain copies the window part.
+// Returns the copy's change of the frame's V (arena parity) past the window:
+// V of the copied bytes at their destination minus V of the bytes they
+// replace in [W, D1). The latter is summed over the shorter of two ranges of
+// original bytes, read before any copy is written (a first pass): [W, D1)
+// itself (kind A), or the frame's bytes after the copy [D1, FE) (kind B),
+// then V(W, D1) = the frame's stream sum - its window chunks - V(D1, FE) -
+// the bytes past its end in its last chunk (cB, from the kept original
+// chunk: in HBM they are the next frame's, whose lane may be rewriting
+// them). Window-only (wo) frames take kind B with cB = 0.
+__device__ __forceinline__ uint32_t coop_payload(bool go, uintptr_t W, uintptr_t D0, uintptr_t D1,
+                                                 uintptr_t FE, uintptr_t src, uint32_t cB,
+                                                 int lane, bool wo, bool defer0) {
+    const uint32_t mw = go ? (uint32_t)(D1 - W) : 0u;    // copied bytes past the window
+    const bool kA = !wo && mw <= (uint32_t)(FE - D1);   // wo frames: kind B (W..D1 never read)
+    const uintptr_t R0 = kA ? W : (D1 & ~(uintptr_t)15);
     const bool rd = go && (kA || FE > D1);             // (a copy to the frame end reads nothing)
-    const uint32_t rlo = rd ? (uint32_t)((kA ? D0 : D1) - R0) : 0u;
+    const uint32_t rlo = rd ? (uint32_t)((kA ? W : D1) - R0) : 0u;
     const uint32_t rhi = rd ? (uint32_t)((kA ? D1 : FE) - R0) : 0u;
     // pass 1: original bytes (loads only)
     const uint32_t vo = wave_segments<SumChunk>(
@@ -1133,78 +1142,68 @@ __device__ __forceinline__ uint32_t coop_payload(bool go, uintptr_t D0, uintptr_
             return c.neg ? 0u - v : v;
         });
     ZB_STAMP(3);
-    // pass 2: the copy
+    // pass 2: the copy, chunks of [D0a, D1); chunk k holds bytes [lo, m)
+    const uintptr_t D0a = D0 & ~(uintptr_t)15;
+    const uint32_t o0 = go ? (uint32_t)(D0 - D0a) : 0u;
+    const uint32_t mc = go ? (uint32_t)(D1 - D0) : 0u;
     const uint32_t vn = wave_segments<CopyChunk>(
-        (mc + 15) >> 4, lane,
+        (o0 + mc + 15) >> 4, lane,
         [&](uint32_t j, uint32_t k, bool live) {
-            const uintptr_t d0 = bperm64(D0, j), s0 = bperm64(src, j);
-            const uint32_t m_all = bperm(mc, j);
+            const uintptr_t d0 = bperm64(D0a, j), s0 = bperm64(src, j);
+            const uint32_t oj = bperm(o0, j), m_all = oj + bperm(mc, j);
             CopyChunk c;
-            c.m = m_all - 16u * k < 16u ? m_all - 16u * k : 16u;
-            const uintptr_t S = s0 + 16u * k, sb = S & ~(uintptr_t)3, send = S + c.m;
-            c.sh = (uint32_t)(S & 3);
+            const uint32_t lo = k == 0 ? oj : 0u;
+            const uint32_t m = m_all - 16u * k < 16u ? m_all - 16u * k : 16u;
+            // source of the chunk's byte 0 (for a first chunk with header
+            // bytes, before src: only dwords holding copied bytes are loaded)
+            const uintptr_t S = s0 + 16u * k - oj, sb = S & ~(uintptr_t)3;
+            const uintptr_t slo = S + lo, send = S + m;
+            const uint32_t sh = (uint32_t)(S & 3);
             c.X = d0 + 16u * k;
-#if ZB_COPY_X4
             // Whole chunks: one dwordx4 from the dword below S; the 5th dword
             // is the next lane's first when it holds this copy's next chunk
-            // (nb), else its own dword load. A copy's last chunk: dword loads
-            // that stop at its end (no read past the blob range).
-            const bool full = c.m == 16;
+            // (nb), else its own dword load. Partial chunks: dword loads
+            // inside the copied range (no read outside the blob range).
+            const bool full = lo == 0 && m == 16;
             const uint32_t jn = bperm(j, (uint32_t)lane + 1u), kn = bperm(k, (uint32_t)lane + 1u);
             const bool ln = bperm(live ? 1u : 0u, (uint32_t)lane + 1u) != 0u;
-            c.nb = lane < 63 && ln && jn == j && kn == k + 1u;
+            const bool nb = lane < 63 && ln && jn == j && kn == k + 1u;
+            c.f = lo | m << 5 | sh << 10 | (nb ? 1u << 12 : 0u);
             if (live && full) {
                 const zp_u32x4 v = *(const ZP_GLOBAL zp_u32x4*)sb;
                 c.x[0] = v.x; c.x[1] = v.y; c.x[2] = v.z; c.x[3] = v.w;
-                c.x[4] = c.sh && !c.nb ? *(const ZP_GLOBAL uint32_t*)(sb + 16u) : 0u;
+                c.x[4] = sh && !nb ? *(const ZP_GLOBAL uint32_t*)(sb + 16u) : 0u;
             } else {
 #pragma unroll
                 for (int u = 0; u < 5; ++u) {
                     const uintptr_t a = sb + 4u * u;
-                    c.x[u] = live && a < send ? *(const ZP_GLOBAL uint32_t*)a : 0u;
+                    c.x[u] = live && a < send && a + 4u > slo ? *(const ZP_GLOBAL uint32_t*)a : 0u;
                 }
             }
-#else
-#pragma unroll
-            for (int u = 0; u < 5; ++u) {
-                const uintptr_t a = sb + 4u * u;
-#if ZB_NT_COPY
-                c.x[u] = live && a < send ? __builtin_nontemporal_load((const ZP_GLOBAL uint32_t*)a) : 0u;
-#else
-                c.x[u] = live && a < send ? *(const ZP_GLOBAL uint32_t*)a : 0u;
-#endif
-            }
-#endif
             return c;
         },
         [&](const CopyChunk& c, uint32_t, uint32_t, bool live) {
-#if ZB_COPY_X4
             const uint32_t x1 = bperm(c.x[0], (uint32_t)lane + 1u);   // every lane (bpermute)
-            const uint32_t x4 = c.m == 16 && c.nb ? x1 : c.x[4];
-#else
-            const uint32_t x4 = c.x[4];
-#endif
+            const uint32_t lo = c.f & 31u, m = (c.f >> 5) & 31u, sh = (c.f >> 10) & 3u;
+            const bool full = lo == 0 && m == 16;
+            const uint32_t x4 = full && (c.f >> 12 & 1u) ? x1 : c.x[4];
             if (!live) return 0u;
-            const uint4 q = make_uint4(__builtin_amdgcn_alignbyte(c.x[1], c.x[0], c.sh),
-                                       __builtin_amdgcn_alignbyte(c.x[2], c.x[1], c.sh),
-                                       __builtin_amdgcn_alignbyte(c.x[3], c.x[2], c.sh),
-                                       __builtin_amdgcn_alignbyte(x4, c.x[3], c.sh));
-            if (c.m == 16) {
-#if ZB_NT_COPY
-                __builtin_nontemporal_store(zp_u32x4{q.x, q.y, q.z, q.w}, (ZP_GLOBAL zp_u32x4*)c.X);
-#else
+            const uint4 q = make_uint4(__builtin_amdgcn_alignbyte(c.x[1], c.x[0], sh),
+                                       __builtin_amdgcn_alignbyte(c.x[2], c.x[1], sh),
+                                       __builtin_amdgcn_alignbyte(c.x[3], c.x[2], sh),
+                                       __builtin_amdgcn_alignbyte(x4, c.x[3], sh));
+            if (full) {
                 *(ZP_GLOBAL zp_u32x4*)c.X = zp_u32x4{q.x, q.y, q.z, q.w};
-#endif
-            } else {
+            } else if (!(defer0 && lo)) {         // (a first chunk with header bytes: the caller)
 #if ZB_WIDE_EDGES
-                store_bytes(c.X, q, 0, c.m);
+                store_bytes(c.X, q, lo, m);
 #else
                 const uint32_t w[4] = {q.x, q.y, q.z, q.w};
-                for (uint32_t b = 0; b < c.m; ++b)
+                for (uint32_t b = lo; b < m; ++b)
                     *(ZP_GLOBAL uint8_t*)(c.X + b) = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
 #endif
             }
-            return range_sum(q, 0, c.m);
+            return range_sum(q, lo, m);
         });
     return vn + (go && !kA ? cB + vo : vo);
 }
@@ -1286,6 +1285,7 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
     bool fast = false;
     bool pay = false;                                  // payload bytes past the window
     uint32_t pay_at = 0, pay_len = 0;
+    bool pay_ovl = false;                              // a TCP payload over its own header
     if (s.live) {
         o0 = pf0;
         const uint32_t o1 = pf1;
@@ -1295,7 +1295,7 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
         // fit it; the copy's bytes past it go straight to HBM after the chain.
         if (o1 >= o0 && len >= 64 && !s.giant) {
 #if ZB_OP_PREFETCH
-            fast = chain_extent(oh, nops, &pay_at, &pay_len) <= s.wlen;
+            fast = chain_extent(oh, nops, &pay_at, &pay_len, &pay_ovl) <= s.wlen;
 #else
             fast = chain_extent(OpGlobal{ops + o0}, nops, &pay_at, &pay_len) <= s.wlen;
 #endif
@@ -1311,6 +1311,10 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
         }
     }
     const OpGlobal og{ops + o0};
+    // ph: the wave copy moves the whole payload (ZB_PAY_HDR), unless it
+    // overwrites the L4 header's own fields (a TCP data offset below 5: the
+    // chain keeps the reference's write order then)
+    const bool ph = ZB_PAY_HDR && pay && !pay_ovl;
     const uint32_t rank = s.rank & 63u;
     const uint32_t nch = (len + s.shift + 15) >> 4;
     WinCsum wc;
@@ -1344,10 +1348,10 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
         wc.region = region;
         BView<uint8_t ZB_LDSP*> v{region + s.shift, len, true};
 #if ZB_LANE_PAY
-        // The chain writes the window's part of the payload; the rest is
-        // copied after it by the whole wave (coop_payload), and the L4
+        // The whole wave copies the payload after the chain (coop_payload;
+        // without ZB_PAY_HDR the chain writes its window part), and the L4
         // checksum is refolded with that copy's V change below.
-        if (pay) v.lim = s.wlen;
+        if (pay) v.lim = ph ? pay_at : s.wlen;
 #endif
 #if ZB_OP_PREFETCH && ZB_OP_KINDS && ZB_LANE_PAY
         err = run_chain<ZB_M_WIN>(v, (const uint8_t ZB_LDSP*)nullptr, s.shift, oh, nops, wc,
@@ -1361,28 +1365,66 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
     {
         // A copy that does not fit the frame failed in the chain before any
         // byte was written (err != 0): nothing to copy then. The headers fit
-        // the window, so the copy starts at the window end (16-B aligned).
+        // the window and the payload reaches past it.
         const bool go = pay && err == 0;
         const uint32_t pe = pay_at + pay_len;
+        const uint32_t c0 = (s.shift + pay_at) >> 4;   // window chunk of the payload's start
         uintptr_t src = 0;
-        uint32_t cB = 0;
+        uint32_t cB = 0, vw = 0;
         if (go) {
-            src = (uintptr_t)data + doff + (s.wlen - pay_at);   // (the chain's last op)
+            src = (uintptr_t)data + doff + (ph ? 0u : s.wlen - pay_at);   // (the chain's last op)
             uint32_t Vw = 0;
 #pragma unroll
-            for (uint32_t c = 0; c < ZP_WIN_CH; ++c) Vw += wc.vorig[c];
+            for (uint32_t c = 0; c < ZP_WIN_CH; ++c) {
+                Vw += wc.vorig[c];
+                // ph: V of the window's bytes from the payload start on, as
+                // the checksum saw them (original bytes, or header bytes an
+                // invalid chain wrote there); the copy's sum has the new ones
+                if (ph && c >= c0)
+                    vw += range_sum(ld_region(region, 16 * c), c == c0 ? (s.shift + pay_at) & 15u : 0u, 16u);
+            }
             const uint32_t he = wo ? 0u : (len + s.shift) & 15u;
             cB = Vw + (he ? range_sum(wc.tail, he, 16u) : 0u) - wc.fsum;   // 0 for wo frames
         }
-        const uint32_t delta = coop_payload(go, s.ga + s.wlen, s.ga + pe, s.ga + len, src, cB,
-                                            lane, wo);
+        const uint32_t delta = coop_payload(go, s.ga + s.wlen, s.ga + (ph ? pay_at : s.wlen),
+                                            s.ga + pe, s.ga + len, src, cB, lane, wo, ZB_PAY_HDR);
         ZB_STAMP(4);
         if (go) {                                      // refold the L4 checksum
             const uint32_t k4 = lkind;                  // the chain's last op (go: all ran)
             const uint32_t at = k4 == ZP_B_TCP ? 16u : k4 == ZP_B_UDP ? 6u : 2u;
-            const uint16_t c = fold_v(wc.cs_V + delta, wc.cs_acc, !((s.ga + wc.cs_l4) & 1));
+            const uint16_t c = fold_v(wc.cs_V + delta - vw, wc.cs_acc, !((s.ga + wc.cs_l4) & 1));
             region[s.shift + wc.cs_l4 + at] = (uint8_t)(c >> 8);
             region[s.shift + wc.cs_l4 + at + 1] = (uint8_t)c;
+#if ZB_PAY_HDR
+            // The chunk holding the payload's first byte, when it also holds
+            // header bytes: those from the region (the checksum refolded),
+            // the payload's from the blob again (a line the copy has just
+            // read), one whole-chunk store.
+            const uint32_t o0 = (s.shift + pay_at) & 15u;
+            if (ph && o0) {
+                const uint4 h = ld_region(region, 16 * c0);
+                const uintptr_t S = src - o0, sb = S & ~(uintptr_t)3;
+                const uint32_t sh2 = (uint32_t)(S & 3);
+                uint32_t x[5];
+#pragma unroll
+                for (int u = 0; u < 5; ++u) {
+                    const uintptr_t a = sb + 4u * u;
+                    x[u] = a < S + 16u && a + 4u > src ? *(const ZP_GLOBAL uint32_t*)a : 0u;
+                }
+                const uint32_t p[4] = {__builtin_amdgcn_alignbyte(x[1], x[0], sh2),
+                                       __builtin_amdgcn_alignbyte(x[2], x[1], sh2),
+                                       __builtin_amdgcn_alignbyte(x[3], x[2], sh2),
+                                       __builtin_amdgcn_alignbyte(x[4], x[3], sh2)};
+                const uint32_t hh[4] = {h.x, h.y, h.z, h.w};
+                uint32_t m[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const uint32_t keep = byte_mask(4 * i, 0, (int)o0);      // header bytes
+                    m[i] = (hh[i] & keep) | (p[i] & ~keep);
+                }
+                *(ZP_GLOBAL zp_u32x4*)((s.ga & ~(uintptr_t)15) + 16u * c0) = zp_u32x4{m[0], m[1], m[2], m[3]};
+            }
+#endif
         }
     }
 #endif
@@ -1409,6 +1451,15 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
         const uint32_t e1 = se < fe ? se : fe;                    // never past the frame
         if (hwc && e1 <= sh + s.wlen) end = e1;                   // bytes in the window
     }
+#endif
+#if ZB_LANE_PAY && ZB_PAY_HDR
+    // the payload's chunks (from the one holding its first byte) are the copy's
+    if (pay_go && ph) {
+        const uint32_t pc = (sh + pay_at) & ~15u;
+        end = end < pc ? end : pc;
+    }
+#endif
+#ifndef ZB_NO_SECTOR_WB
     // the previous lane's frame and where its writes end (all lanes active)
 #if ZB_LANE_PAY
     const uintptr_t wend = pay_go ? s.ga + pay_at + pay_len : a0 + end;
