@@ -955,6 +955,12 @@ __device__ __forceinline__ uint32_t chain_extent(const Ops& ops, uint32_t nops, 
 #if ZB_SKIP_PAY && !(ZB_LANE_PAY && ZB_OP_PREFETCH)
 #error "ZB_SKIP_PAY needs ZB_LANE_PAY and ZB_OP_PREFETCH"
 #endif
+#ifndef ZB_MARK
+#define ZB_MARK 1              // V of the bytes a copy replaces from the stream (no first pass)
+#endif
+#if ZB_MARK && defined(ZB_NO_SECTOR_WB)
+#error "ZB_MARK needs the T4 stream"
+#endif
 #ifndef ZB_PAY_HDR
 #define ZB_PAY_HDR 1           // the wave copy moves the whole payload (the chain copies none of it)
 #endif
@@ -1115,11 +1121,14 @@ struct SumChunk { uint4 q; uint32_t l, h, neg; };
 // them). Window-only (wo) frames take kind B with cB = 0.
 __device__ __forceinline__ uint32_t coop_payload(bool go, uintptr_t W, uintptr_t D0, uintptr_t D1,
                                                  uintptr_t FE, uintptr_t src, uint32_t cB,
-                                                 int lane, bool wo, bool defer0) {
+                                                 int lane, bool wo, bool defer0,
+                                                 bool known = false, uint32_t vrep = 0) {
     const uint32_t mw = go ? (uint32_t)(D1 - W) : 0u;    // copied bytes past the window
     const bool kA = !wo && mw <= (uint32_t)(FE - D1);   // wo frames: kind B (W..D1 never read)
     const uintptr_t R0 = kA ? W : (D1 & ~(uintptr_t)15);
-    const bool rd = go && (kA || FE > D1);             // (a copy to the frame end reads nothing)
+    // (known: V(W, D1) is vrep, from the stream; a copy to the frame end
+    // reads nothing either)
+    const bool rd = go && !known && (kA || FE > D1);
     const uint32_t rlo = rd ? (uint32_t)((kA ? W : D1) - R0) : 0u;
     const uint32_t rhi = rd ? (uint32_t)((kA ? D1 : FE) - R0) : 0u;
     // pass 1: original bytes (loads only)
@@ -1205,7 +1214,7 @@ __device__ __forceinline__ uint32_t coop_payload(bool go, uintptr_t W, uintptr_t
             }
             return range_sum(q, lo, m);
         });
-    return vn + (go && !kA ? cB + vo : vo);
+    return vn + (known ? 0u - vrep : go && !kA ? cB + vo : vo);
 }
 
 #ifdef ZB_FAST_WPE_MAX
@@ -1223,9 +1232,11 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
     // the 3 chunks before each frame's last one (the previous frame's bytes
     // in a frame's first 64-B sector)
     __shared__ uint4 t4[64 * ZP_T4N];
+    __shared__ uint32_t cmid[64];                      // running sum at each frame's mark
     constexpr bool T4 = true;
 #else
     uint4* t4 = nullptr;
+    uint32_t* cmid = nullptr;
     constexpr bool T4 = false;
 #endif
     const int lane = threadIdx.x & 63;
@@ -1253,7 +1264,11 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
     // the copy replaces are never read, the ones after it are read by the
     // copy's first pass, and the L4 sum is built from the new window, the
     // copy and those. Deciding it needs the chain's heads before the stream.
+    // The other payload frames mark the copy's end in the stream (ZB_MARK):
+    // the running sum there gives V of the bytes the copy replaces, so the
+    // copy needs no first pass over them.
     bool wo = false;
+    uint32_t mark = ~0u;
     if (ip < n && pf1 >= pf0 && len >= 64 && len <= ZP_GIANT) {
         uint32_t pa = 0, pl = 0;
         const uint32_t sh0 = (uint32_t)(ga & 15);
@@ -1261,20 +1276,22 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
         if (chain_extent(oh, pf1 - pf0, &pa, &pl) <= wl0 && pl && pa + pl > wl0) {
             const uint32_t pe = pa + pl;
             wo = pe <= len && pe - wl0 >= len - pe;
+            if (ZB_MARK && !wo && pe < len) mark = pe;
         }
     }
-    tile_setup(s, t, len, ga, n, lane, lds, wo);
+    tile_setup(s, t, len, ga, n, lane, lds, wo, mark);
 #else
     const bool wo = false;
+    const uint32_t mark = ~0u;
     tile_setup(s, t, len, ga, n, lane, lds);
 #endif
     uint4 va[ZP_G];
     uint32_t ka[ZP_G];
     issue_group<ZP_G, T4>(0, s.nitems, s.cur, s.R, lane, fallback, va, ka);
-    consume_group<ZP_G, T4>(0, s.nitems, lane, va, ka, win, tail, lds.cend, s.run, t4);
+    consume_group<ZP_G, T4>(0, s.nitems, lane, va, ka, win, tail, lds.cend, s.run, t4, cmid);
     for (uint32_t i0 = ZP_G; i0 < s.nitems; i0 += ZP_G) {
         issue_group<ZP_G, T4>(i0, s.nitems, s.cur, s.R, lane, fallback, va, ka);
-        consume_group<ZP_G, T4>(i0, s.nitems, lane, va, ka, win, tail, lds.cend, s.run, t4);
+        consume_group<ZP_G, T4>(i0, s.nitems, lane, va, ka, win, tail, lds.cend, s.run, t4, cmid);
     }
     wave_lds_fence();                                  // windows written by other lanes
     ZB_STAMP(1);
@@ -1370,10 +1387,9 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
         const uint32_t pe = pay_at + pay_len;
         const uint32_t c0 = (s.shift + pay_at) >> 4;   // window chunk of the payload's start
         uintptr_t src = 0;
-        uint32_t cB = 0, vw = 0;
+        uint32_t cB = 0, vw = 0, Vw = 0;
         if (go) {
             src = (uintptr_t)data + doff + (ph ? 0u : s.wlen - pay_at);   // (the chain's last op)
-            uint32_t Vw = 0;
 #pragma unroll
             for (uint32_t c = 0; c < ZP_WIN_CH; ++c) {
                 Vw += wc.vorig[c];
@@ -1386,8 +1402,13 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
             const uint32_t he = wo ? 0u : (len + s.shift) & 15u;
             cB = Vw + (he ? range_sum(wc.tail, he, 16u) : 0u) - wc.fsum;   // 0 for wo frames
         }
+        // a marked frame: V of the original bytes [W, D1) from the running
+        // sum at the copy's end minus the frame's start and window chunks
+        const bool known = ZB_MARK && go && mark != ~0u;
+        const uint32_t vrep = known ? cmid[rank] - (rank ? lds.cend[rank - 1] : 0u) - Vw : 0u;
         const uint32_t delta = coop_payload(go, s.ga + s.wlen, s.ga + (ph ? pay_at : s.wlen),
-                                            s.ga + pe, s.ga + len, src, cB, lane, wo, ZB_PAY_HDR);
+                                            s.ga + pe, s.ga + len, src, cB, lane, wo, ZB_PAY_HDR,
+                                            known, vrep);
         ZB_STAMP(4);
         if (go) {                                      // refold the L4 checksum
             const uint32_t k4 = lkind;                  // the chain's last op (go: all ran)

@@ -144,6 +144,7 @@ struct Ranked {          // lane r = frame of rank r
     uint32_t org_lo, org_hi;   // (A & ~15) - 16 * pfx
     uint32_t last;       // last virtual chunk
     uint32_t pfx;        // first virtual chunk
+    uint32_t mid;        // T4 streams: (virtual chunk << 4) | byte of a marked frame offset, or ~0
 };
 
 // Per-lane item descriptor.
@@ -155,6 +156,8 @@ struct Ranked {          // lane r = frame of rank r
 #endif
 #define KEEP_T4 (1u << 28)     // one of the ZP_T4N chunks before the frame's last (T4 streams) ...
 #define KEEP_T4D(k) (((k) >> 22) & 3u)   // ... at this distance from the last, minus 1
+#define KEEP_MID (1u << 27)    // (T4 streams) the chunk of the frame's marked offset, its byte in 10-13
+#define KEEP_MIDB(k) (((k) >> 10) & 15u)
 #define KEEP_CELL(k) ((k) & 0x3FFu)
 #define KEEP_RANK(k) (((k) >> 16) & 63u)
 
@@ -236,7 +239,11 @@ __device__ __forceinline__ void issue_group(uint32_t i0, uint32_t nitems, Cursor
         uint32_t k = (r & 63u) << 16;
         k |= ci < ZP_WIN_CH ? KEEP_WIN | (ci * 64u + ((r ^ ci) & 63u)) : 0u;
         k |= vv == lv ? KEEP_TAIL : 0u;
-        if (T4) k |= lv - vv - 1u < (uint32_t)ZP_T4N ? KEEP_T4 | ((lv - vv - 1u) << 22) : 0u;
+        if (T4) {
+            k |= lv - vv - 1u < (uint32_t)ZP_T4N ? KEEP_T4 | ((lv - vv - 1u) << 22) : 0u;
+            const uint32_t md = bperm(R.mid, r);
+            k |= (md >> 4) == vv ? KEEP_MID | ((md & 15u) << 10) : 0u;
+        }
         keep[q] = (i < nitems && vv <= lv) ? k | KEEP_IN : 0u;
         const uint32_t vc = vv < lv ? vv : lv;
         a[q] = nitems ? (((uintptr_t)ohi << 32) | olo) + 16ull * vc : fallback;
@@ -262,7 +269,8 @@ template <int G, bool T4 = false>
 __device__ __forceinline__ void consume_group(uint32_t i0, uint32_t nitems, int lane,
                                               const uint4 (&v)[G], const uint32_t (&keep)[G],
                                               uint4* win, uint4* tail, uint32_t* cend,
-                                              uint32_t& run, uint4* t4 = nullptr) {
+                                              uint32_t& run, uint4* t4 = nullptr,
+                                              uint32_t* cmid = nullptr) {
     // Items past the end (wave-uniform) are skipped by a branch, not a
     // loop exit: with `break` LLVM stops fully unrolling past G = 8 and the
     // group arrays go to scratch.
@@ -292,6 +300,9 @@ __device__ __forceinline__ void consume_group(uint32_t i0, uint32_t nitems, int 
             tail[KEEP_RANK(k)] = v[q];
             cend[KEEP_RANK(k)] = run + P;
         }
+        // T4 streams: the running sum through the marked byte of a frame
+        // (its chunks before it and the chunk's bytes before the mark)
+        if (T4 && (k & KEEP_MID)) cmid[KEEP_RANK(k)] = run + P - part + range_sum(v[q], 0u, KEEP_MIDB(k));
         run += rdl(P, 63);
     }
     // Retire the dummy loads of a short last group here: a load still in
@@ -324,7 +335,7 @@ struct TileState {
 // len = 0 lanes (past the batch) own no chunks.
 __device__ __forceinline__ void tile_setup(TileState& s, uint64_t tile, uint32_t len,
                                            uintptr_t ga, uint64_t n, int lane, WaveLds& lds,
-                                           bool win_only = false) {
+                                           bool win_only = false, uint32_t mark = ~0u) {
     s.tile = tile;
     s.ga = ga;
     s.len = len;
@@ -354,6 +365,10 @@ __device__ __forceinline__ void tile_setup(TileState& s, uint64_t tile, uint32_t
     s.R.org_hi = (uint32_t)__builtin_amdgcn_ds_permute(a, (int)(uint32_t)(org >> 32));
     s.R.last = (uint32_t)__builtin_amdgcn_ds_permute(a, (int)(incl - 1));
     s.R.pfx = (uint32_t)__builtin_amdgcn_ds_permute(a, (int)pfx);
+    // a marked frame offset (T4 streams) inside the streamed chunks
+    const uint32_t mc = mark != ~0u && nch ? (s.shift + mark) >> 4 : ~0u;
+    const uint32_t mid = mc < nch ? ((pfx + mc) << 4) | ((s.shift + mark) & 15u) : ~0u;
+    s.R.mid = (uint32_t)__builtin_amdgcn_ds_permute(a, (int)mid);
     s.cur.rbase = ~0u;
     s.cur.nz = nz;
     s.cur.starts = &lds.starts[0];
