@@ -27,9 +27,15 @@ def main():
                     help="offsets of arena copies within one pool (records fixed)")
     ap.add_argument("--arena-allocs", type=int, default=0,
                     help="separate allocations of arena copies (records fixed)")
+    ap.add_argument("--hip-allocs", default="",
+                    help="arena copies in hipMalloc / hipExtMallocWithFlags buffers: "
+                         "comma list of default,contig")
+    ap.add_argument("--dummy-first", type=int, default=0,
+                    help="GiB allocated (and kept) before the arena is generated")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     n = args.frames
+    dummy = torch.empty(args.dummy_first << 30, dtype=torch.uint8, device=dev) if args.dummy_first else None
     arena, offs, lens = zp.batch.generate("c3", n, device=dev)
     ext = torch.empty((2, n, 16), dtype=torch.uint8, device=dev)
 
@@ -100,6 +106,32 @@ def main():
             ms = float(np.median(out[i]))
             print(f"arena alloc {i} (VA {c.data_ptr():#x}): {ms:.3f} ms = {total / ms / 1e6 / 8000:.3f}  "
                   f"rounds {['%.3f' % x for x in out[i]]}", flush=True)
+    if args.hip_allocs:
+        hip = ctypes.CDLL("libamdhip64.so")
+        hip.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
+        hip.hipExtMallocWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_uint]
+        hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        hip.hipFree.argtypes = [ctypes.c_void_p]
+        bufs = []
+        for kind in args.hip_allocs.split(","):
+            p = ctypes.c_void_p()
+            rc = (hip.hipMalloc(ctypes.byref(p), nbytes) if kind == "default" else
+                  hip.hipExtMallocWithFlags(ctypes.byref(p), nbytes, 0x4))
+            if rc != 0:
+                print(f"{kind}: allocation failed rc {rc}", flush=True)
+                continue
+            assert hip.hipMemcpy(p, ctypes.c_void_p(arena.data_ptr()), nbytes, 3) == 0   # device to device
+            bufs.append((kind, p.value))
+        out = [[] for _ in bufs]
+        for _ in range(args.rounds):
+            for i, (_, a) in enumerate(bufs):
+                out[i].append(timed(a, pool.data_ptr()))
+        for i, (kind, a) in enumerate(bufs):
+            ms = float(np.median(out[i]))
+            print(f"hip {kind} alloc (VA {a:#x}): {ms:.3f} ms = {total / ms / 1e6 / 8000:.3f}  "
+                  f"rounds {['%.3f' % x for x in out[i]]}", flush=True)
+        for _, a in bufs:
+            hip.hipFree(ctypes.c_void_p(a))
     for o in offsets:
         ms = float(np.median(res[o]))
         print(f"records at pool+{o:>10} (rec-arena {(pool.data_ptr() + o - arena.data_ptr()) % (1 << 30):#x} mod 1G): "
