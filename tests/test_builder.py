@@ -539,3 +539,58 @@ def test_gpu_builder_payload_copies(zp, P, gap):
     assert got.tobytes() == wres.tobytes()
     errs = {int(e) for e in wres["err"]}
     assert 0 in errs and len(errs) >= 2, sorted(errs)
+
+
+@pytest.mark.gpu
+def test_gpu_builder_payload_overlaps(zp):
+    """Payloads past the window behind chains whose writes overlap (the wave
+    copy moves the whole payload, zp_build.hip ZB_PAY_HDR): a TCP data offset
+    below 5 (the payload overwrites its own header, then the checksum the
+    payload; tcp.rs:108-114, builder.rs:473-474), an IPv4 IHL of 0 (the L4
+    header and payload overwrite the IPv4 header), authentication data longer
+    than its header (authentication.rs:84-92) under a payload that fits and
+    one that does not (ICMPV6_PAYLOAD); every frame start offset mod 16, every
+    byte, header_len and error identical to the oracle."""
+    import torch
+    rng = random.Random(99)
+    C = zp.builder.Chain
+    chains, lens, fills = [], [], []
+    for k in range(16 * 24):
+        kind = k % 4
+        c = C().ethernet(rb(rng, 6), rb(rng, 6), 0x86DD if kind >= 2 else 0x0800)
+        pay = bytes(rb(rng, rng.randrange(90, 400)))
+        if kind == 0:                                   # TCP data offset 0 or 2
+            c.ipv4(4, 5, 0, 0, 60, 1, 0, 0, 64, 6, rb(rng, 4), rb(rng, 4))
+            c.tcp(rb(rng, 4), 1, rb(rng, 4), 2, 3, 4, rng.choice([0, 2]), 0, 0x18, 9, 0, pay)
+            need = 14 + 20 + 20 + len(pay)
+        elif kind == 1:                                 # IPv4 IHL 0
+            c.ipv4(4, 0, 0, 0, 60, 1, 0, 0, 64, 17, rb(rng, 4), rb(rng, 4))
+            c.udp(rb(rng, 4), 1, rb(rng, 4), 2, 8 + len(pay), pay)
+            need = 14 + 20 + len(pay)
+        else:                                           # AH data past its header length
+            c.ipv6(6, 0, 0, 0, 51, 64, rb(rng, 16), rb(rng, 16))
+            c.authentication_header(58, 1, rng.randrange(1 << 32), rng.randrange(1 << 32),
+                                    rb(rng, rng.randrange(8, 40)))
+            c.icmpv6(rb(rng, 16), rb(rng, 16), 128, 0, pay)
+            need = 14 + 40 + 12 + 8 + len(pay)
+        size = need + rng.randrange(0, 200) if kind != 3 else need - rng.randrange(1, 60)
+        chains.append(c); lens.append(max(size, 64))
+        fills.append(np.array(rb(rng, max(size, 64)), np.uint8))
+    before, want, offs, lens_, wres, _ = run_oracle(zp, chains, lens, fill=fills, align=1, gap=1)
+    assert len({int(o) % 16 for o in offs}) == 16
+    d = torch.device("cuda:0")
+    arena = torch.from_numpy(before).to(d)
+    batch = zp.builder.BuildBatch()
+    for c in chains:
+        batch.add(c)
+    got = batch.run(arena, torch.from_numpy(offs.astype(np.int64)).to(d),
+                    torch.from_numpy(lens_.astype(np.int32)).to(d))
+    torch.cuda.synchronize()
+    ga = arena.cpu().numpy()
+    bad = [i for i, (o, l_) in enumerate(zip(offs, lens_))
+           if ga[o:o + l_].tobytes() != want[o:o + l_].tobytes()]
+    assert not bad, (len(bad), bad[:5], [int(wres[i]["err"]) for i in bad[:5]])
+    assert ga.tobytes() == want.tobytes()
+    assert got.tobytes() == wres.tobytes()
+    errs = {int(e) for e in wres["err"]}
+    assert 0 in errs and len(errs) >= 2, sorted(errs)
