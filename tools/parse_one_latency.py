@@ -18,12 +18,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--calls", type=int, default=3000)
     ap.add_argument("--threads", default="1,8")
+    ap.add_argument("--lib", default="", help="directory of another libzp_hip.so build (A/B)")
     args = ap.parse_args()
     zp = importlib.import_module("zero-packet_amd")
     a, o, l_ = zp.batch.generate_host("c3", 256)
     frames = "".join(a[x:x + y].tobytes().hex() + "\n" for x, y in zip(o, l_))
-    lib = os.path.join(ROOT, "zero-packet_amd")
-    exe = os.path.join(ROOT, "tools", "latency", "parse_one")
+    lib = os.path.abspath(args.lib) if args.lib else os.path.join(ROOT, "zero-packet_amd")
+    exe = os.path.join(ROOT, "tools", "latency", "parse_one" + ("_ab" if args.lib else ""))
     subprocess.run(["g++", "-std=c++17", "-O2", "-pthread", "-I", os.path.join(ROOT, "include"),
                     "-o", exe, os.path.join(ROOT, "tools", "latency", "parse_one_main.cpp"),
                     "-L" + lib, "-lzp_hip", "-Wl,-rpath," + lib], check=True)
