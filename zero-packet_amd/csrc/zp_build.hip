@@ -172,10 +172,6 @@ __device__ __forceinline__ void wave_sync() {
 // LDS layout (the lane-per-frame path, zp_build_fast_kernel).
 enum { ZB_M_COOP = 0, ZB_M_GLOBAL = 1, ZB_M_WIN = 2 };
 
-#ifndef ZB_WIN_COPY_DW
-#define ZB_WIN_COPY_DW 0       // 1: ZB_M_WIN blob copies by dword loads (chain phase -22 %, kernel
-                               // P = 1000 0, P = 200 +2.3 %: r04_build_wincopy_ab.log)
-#endif
 
 // Copies `len` bytes of the data blob to frame offset `at`.
 template <int MODE, typename P>
@@ -213,54 +209,11 @@ __device__ void bcopy(BView<P>& v, uint32_t at, const uint8_t* src, uint32_t len
     } else if constexpr (MODE == ZB_M_WIN) {
         // the part inside the lane's window; a payload past it goes to HBM
         // after the chain (zp_build_fast_kernel)
-#ifdef ZB_ABL_NOWINCOPY
-        const uint32_t m = 0;                        // timing probe only: no window part
-#else
         // (only the final payload copy is cut: extension data lies inside
         // the chain's extent, which the window holds)
         const uint32_t lim = payload ? v.lim : ~0u;
         const uint32_t m = at >= lim ? 0u : (lim - at < len ? lim - at : len);
-#endif
-#if ZB_WIN_COPY_DW
-        // Dword-aligned blob loads (address space 1, 9 in flight), realigned
-        // to the destination's dwords with alignbyte: whole dwords by one LDS
-        // store, the edges byte by byte. Loads touch only dwords holding
-        // bytes of [src, src + m).
-        if (!m) return;
-        uint8_t ZB_LDSP* dst = (uint8_t ZB_LDSP*)(v.b + at);
-        const uint32_t dmis = (uint32_t)(size_t)dst & 3u;
-        uint32_t ZB_LDSP* dw = (uint32_t ZB_LDSP*)(dst - dmis);
-        const uintptr_t lo = (uintptr_t)src, hi = lo + m;
-        const uintptr_t S0 = lo - dmis;                  // source of dst dword 0's first byte
-        const uint32_t sh = (uint32_t)(S0 & 3u);
-        const uintptr_t g0 = S0 & ~(uintptr_t)3;
-        const uint32_t nw = (dmis + m + 3) >> 2;
-        for (uint32_t w0 = 0; w0 < nw; w0 += 8) {
-            uint32_t x[9];
-#pragma unroll
-            for (uint32_t u = 0; u < 9; ++u) {
-                const uintptr_t a = g0 + 4u * (w0 + u);
-                x[u] = w0 + u <= nw && a + 4u > lo && a < hi ? *(const ZP_GLOBAL uint32_t*)a : 0u;
-            }
-#pragma unroll
-            for (uint32_t u = 0; u < 8; ++u) {
-                const uint32_t w = w0 + u;
-                if (w < nw) {
-                    const uint32_t val = __builtin_amdgcn_alignbyte(x[u + 1], x[u], sh);
-                    const int p0 = (int)(4u * w) - (int)dmis;
-                    if (p0 >= 0 && p0 + 4 <= (int)m) {
-                        dw[w] = val;
-                    } else {
-#pragma unroll
-                        for (int b = 0; b < 4; ++b)
-                            if (p0 + b >= 0 && p0 + b < (int)m) dst[p0 + b] = (uint8_t)(val >> (8 * b));
-                    }
-                }
-            }
-        }
-#else
         for (uint32_t q = 0; q < m; ++q) v.b[at + q] = src[q];
-#endif
     } else {
         for (uint32_t q = 0; q < len; ++q) v.b[at + q] = src[q];
     }
@@ -744,62 +697,6 @@ struct OpGlobal {
 #ifndef ZB_OPH
 #define ZB_OPH 4
 #endif
-#ifndef ZB_OP_FULL
-#define ZB_OP_FULL 0           // 1: the first 3 ops whole in registers from before the stream
-#endif
-#if ZB_OP_FULL
-// The first 3 ops whole, loaded once before the stream (each op line is read
-// once; with heads only, the ops are read again after the stream). Three
-// named ops, selected with ternaries: an array indexed by k goes to scratch.
-struct OpQ { zp_u32x4 a, b, c, d; };
-struct OpHeads {
-    OpGlobal og;
-    OpQ f0, f1, f2;
-    __device__ __forceinline__ static OpQ ld(const zp_build_op* g, bool on) {
-        const ZP_GLOBAL zp_u32x4* q = (const ZP_GLOBAL zp_u32x4*)g;
-        const zp_u32x4 z{0, 0, 0, 0};
-        OpQ o;
-        o.a = on ? q[0] : z; o.b = on ? q[1] : z; o.c = on ? q[2] : z; o.d = on ? q[3] : z;
-        return o;
-    }
-    __device__ __forceinline__ void load(uint32_t nops) {
-        f0 = ld(og.g, nops > 0);
-        f1 = ld(og.g + (nops > 1 ? 1 : 0), nops > 1);
-        f2 = ld(og.g + (nops > 2 ? 2 : 0), nops > 2);
-    }
-    // (the values pass an empty asm first: a select of loads from one
-    // aggregate would otherwise become one load at a computed address, and
-    // the aggregate would live in scratch)
-    __device__ __forceinline__ static zp_u32x4 pick(uint32_t k, zp_u32x4 x, zp_u32x4 y, zp_u32x4 z) {
-        asm volatile("" : "+v"(x), "+v"(y), "+v"(z));
-        return k == 0 ? x : k == 1 ? y : z;
-    }
-    __device__ __forceinline__ OpQ sel(uint32_t k) const {
-        OpQ o;
-        o.a = pick(k, f0.a, f1.a, f2.a);
-        o.b = pick(k, f0.b, f1.b, f2.b);
-        o.c = pick(k, f0.c, f1.c, f2.c);
-        o.d = pick(k, f0.d, f1.d, f2.d);
-        return o;
-    }
-    __device__ __forceinline__ uint2 head(uint32_t k) const {
-        if (k >= 3) return og.head(k);
-        const OpQ o = sel(k);
-        return make_uint2(o.a.x, o.b.w);
-    }
-    __device__ __forceinline__ zp_build_op get(uint32_t k) const {
-        OpQ q = sel(k);
-        if (k >= 3) q = ld(og.g + k, true);
-        const zp_u32x4 t[4] = {q.a, q.b, q.c, q.d};
-        zp_build_op o;
-        __builtin_memcpy(&o, t, sizeof o);
-        return o;
-    }
-    __device__ __forceinline__ uint32_t kind(uint32_t k) const {
-        return k < 3 ? (head(k).x & 0xFFu) : og.kind(k);
-    }
-};
-#else
 struct OpHeads {
     OpGlobal og;
     uint2 h[ZB_OPH];
@@ -819,7 +716,6 @@ struct OpHeads {
         return k < ZB_OPH ? (head(k).x & 0xFFu) : og.kind(k);
     }
 };
-#endif
 #ifndef ZB_OP_KINDS
 #define ZB_OP_KINDS 1          // run_chain's typestate pass reads the prefetched kinds
 #endif
@@ -1217,12 +1113,7 @@ __device__ __forceinline__ uint32_t coop_payload(bool go, uintptr_t W, uintptr_t
     return vn + (known ? 0u - vrep : go && !kA ? cB + vo : vo);
 }
 
-#ifdef ZB_FAST_WPE_MAX
-#define ZB_FAST_WPE_ATTR amdgpu_waves_per_eu(ZB_FAST_WPE, ZB_FAST_WPE_MAX)
-#else
-#define ZB_FAST_WPE_ATTR amdgpu_waves_per_eu(ZB_FAST_WPE)
-#endif
-__global__ void __launch_bounds__(64) __attribute__((ZB_FAST_WPE_ATTR))
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ZB_FAST_WPE)))
 zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs,
                      const uint32_t* __restrict__ lens, uint64_t n,
                      const zp_build_op* __restrict__ ops, const uint32_t* __restrict__ op_start,
