@@ -24,7 +24,10 @@
 extern "C" char* zp__errbuf(void);
 
 #ifndef FX_WIN
-#define FX_WIN 160                       // staged bytes per frame (from A & ~15): covers c4 headers
+#define FX_WIN 112                       // staged bytes per frame (from A & ~15); longer headers
+                                         // (some c4 chains) read the rest from HBM. 112 vs 160:
+                                         // c3 -5 %, c5 -9 %, c4 +-2 % (28 KB of LDS per workgroup
+                                         // instead of 40: more workgroups per CU; r04_cols_window_ab.log)
 #endif
 #define FX_CH (FX_WIN / 16)
 #define FX_BLOCK 256
