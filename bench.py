@@ -27,7 +27,8 @@ Reported next to the GPU number:
                 (rank 0 at N = 1 only)
   h2d_d2h_inclusive  host-pinned frames -> H2D -> parse -> D2H (PCIe) rate on
                 a 2M-frame sample (zp_parse_batch_host), every rank at once,
-                frames summed over ranks / the slowest rank; never `value`
+                frames summed over ranks / the slowest rank; never `value`;
+                rejected frames reported, not asserted
   config5       BASELINE config 5 in the same ranks after the headline: the
                 256M-frame IMIX stream (--c5-frames) cut into N contiguous
                 shards (strong scaling), its own timed loop of --steps
@@ -194,8 +195,7 @@ def pcie_inclusive(zp, arena, offs, lens, sample_pkts, barrier=lambda: None):
     barrier()
     lib.zp_ctx_destroy(ctx)
     errs = int((zp.batch.record_err(recs) != 0).sum().item())
-    assert errs == 0, f"host path: {errs} frames rejected"
-    return m, end, sec
+    return m, end, sec, errs
 
 
 PCIE_PATH = "pinned host -> H2D -> kernel -> D2H records, 2 streams x 256 MiB chunks"
@@ -388,14 +388,15 @@ def main():
     coll_dev = "cpu" if shared else dev
     if not args.no_pcie:
         # every rank's host path at once: frames of all ranks / the slowest rank
-        m, nb, sec = pcie_inclusive(zp, arena, offs, lens, 1 << 21, barrier)
-        rows = gather_rows([m, nb, sec], world, rank, coll_dev)
+        m, nb, sec, perr = pcie_inclusive(zp, arena, offs, lens, 1 << 21, barrier)
+        rows = gather_rows([m, nb, sec, perr], world, rank, coll_dev)
         t = float(rows[:, 2].max())
         out["h2d_d2h_inclusive"] = {
             "mpkt_per_s": round(float(rows[:, 0].sum()) / t / 1e6, 2),
             "gb_per_s": round(float(rows[:, 1].sum()) / t / 1e9, 2),
             "sample_frames": int(rows[:, 0].sum()), "ranks": world,
             "per_rank_gb_per_s": [round(float(b) / s / 1e9, 2) for b, s in rows[:, 1:3]],
+            "rejected_frames": int(rows[:, 3].sum()),
             "path": PCIE_PATH + ("; all ranks concurrently, summed" if world > 1 else "")}
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(zp, arena, offs, lens, args.cpu_sample,
@@ -411,7 +412,8 @@ def main():
         torch.cuda.empty_cache()
         out["config5"] = config5_leg(zp, parse_count(args.c5_frames), args.steps, args.warmup,
                                      world, rank, dev, barrier, coll_dev)
-        assert sum(out["config5"]["rejected_per_rank"]) == 0, "config 5: frames rejected"
+        # rejected frames are reported (rejected_per_rank), not asserted: the
+        # generator writes valid frames, so a nonzero count is a finding
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -324,17 +324,25 @@ int zp_parse_batch_host_multi(zp_ctx* const* ctxs, int nctx, const uint8_t* aren
                               uint64_t arena_bytes, const uint64_t* offs,
                               const uint32_t* lens, uint64_t n, zp_record* records,
                               zp_ext_offsets* ext);
-/* One frame through the GPU path (PacketParser::parse equivalent). ext: NULL
- * or 2 entries (outer, ip_in_ip chain; zeroed where the record flags no
- * chain). Returns the zp_err code (>= 0) or a negative value on HIP failure.
- * Latency, not throughput: the frame is copied into ctx's mapped pinned
- * block, the kernel reads it and writes the record there, and the call
- * waits (~20 us per call on MI355X; the CPU reference
- * parses a frame in well under 1 us). Callers with a stream of frames
- * should batch them: the host ring (zp_ring_*) or zp_parse_batch_host /
- * zp_parse_batch_device. Frames over 64 KiB take the batch host path. */
+/* One frame through the GPU path (PacketParser::parse equivalent,
+ * parser.rs:53). ext: NULL or 2 entries (outer, ip_in_ip chain; zeroed where
+ * the record flags no chain). Returns the zp_err code (>= 0) or a negative
+ * value on HIP failure. The frame is copied into ctx's mapped pinned block;
+ * by default a resident server wave of ctx (one wave on one CU, launched on
+ * the first call) polls a doorbell there, parses the frame in place and
+ * writes the record back: no kernel launch per call.
+ * The wave leaves after an idle timeout (5 ms by default) without requests
+ * and is relaunched by the next call. While it runs, a device-wide
+ * synchronisation (hipDeviceSynchronize, torch.cuda.synchronize, hipFree)
+ * waits for it to leave: call zp_parse_one_config first to stop it at once.
+ * Frames over 64 KiB take the batch host path. */
 int zp_parse_one(zp_ctx* ctx, const uint8_t* frame, uint64_t len,
                  zp_record* record, zp_ext_offsets ext[2]);
+/* zp_parse_one's mode on ctx: idle_us > 0 = the resident server with that
+ * idle timeout (the default is 5000); 0 = one batch-kernel launch and a
+ * stream wait per call (~18 us). Stops a running server either way.
+ * Returns 0, or -1 on a NULL ctx. */
+int zp_parse_one_config(zp_ctx* ctx, uint32_t idle_us);
 
 /* ------------------------------------------------------------------------- */
 /* Standalone readers and the checksum primitives.                           */

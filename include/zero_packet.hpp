@@ -459,12 +459,19 @@ struct PacketParser {
         if (zp_rec_is_far(r)) {
             // (zp_rec_decode restated, header-only) ethernet.rs:155-179, then
             // the ip_in_ip header behind the outer IP header
-            if (!(flags & ZP_F_IP_IN_IP) || frame.len < 62)
+            if (!(flags & ZP_F_IP_IN_IP))
                 throw std::invalid_argument("from_record: far-L4 record without ip_in_ip");
+            // the offsets the record implies must lie in the frame (as zp_rec_decode checks)
+            if (zp_rec_l4_off(r) >= frame.len || frame.len < 14)
+                throw std::invalid_argument("from_record: frame too short for the record");
             const uint32_t t = detail::be16(frame, 12);
             hl = t == 0x8100 ? 18 : t == 0x88A8 ? 22 : 14;
+            if (hl >= frame.len)
+                throw std::invalid_argument("from_record: frame too short for the record");
             io = (flags & ZP_F_IPV6) ? hl + 40 + ((flags & ZP_F_EXT) ? outer->len : 0)
                                      : hl + (frame[hl] & 15u) * 4;   // ipv4.rs:228-258
+            if (io >= frame.len)
+                throw std::invalid_argument("from_record: frame too short for the record");
         }
         if (flags & ZP_F_ETHERNET) p.ethernet.emplace(frame, hl);
         if (flags & ZP_F_ARP) p.arp.emplace(frame.sub(hl));
@@ -526,6 +533,9 @@ public:
         if (!ctx_) throw std::runtime_error(std::string("zp_ctx_create: ") + zp_last_error());
     }
     ~Context() { zp_ctx_destroy(ctx_); }
+    // zp_parse_one's mode: idle_us > 0 = resident server (default 5000 us
+    // idle timeout), 0 = one launch per call; stops a running server.
+    void parse_one_mode(uint32_t idle_us) { zp_parse_one_config(ctx_, idle_us); }
     Context(const Context&) = delete;
     Context& operator=(const Context&) = delete;
     zp_ctx* get() const { return ctx_; }

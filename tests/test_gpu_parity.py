@@ -716,9 +716,10 @@ def test_mixed_stack_path_mutations(zp):
 
 def test_parse_one_sizes(zp):
     """zp_parse_one on both of its paths: frames up to 64 KiB through the
-    mapped block (the kernel reads the frame and writes the record over the
-    host link), longer ones through the batch host path; records and chains
-    equal the oracle's, unflagged chain entries zero."""
+    mapped block (the resident server wave, then one batch launch per call,
+    read the frame and write the record over the host link), longer ones
+    through the batch host path; records and chains equal the oracle's,
+    unflagged chain entries zero."""
     import ctypes
     rng = np.random.default_rng(13)
     a, o, l_ = zp.batch.generate_host("c4", 40, first=77)
@@ -729,14 +730,63 @@ def test_parse_one_sizes(zp):
     lib = zp._lib.hip()
     ctx = lib.zp_ctx_create(0, 0)
     try:
-        for f in frames:
-            rec = np.zeros(1, zp.records.RECORD_DTYPE)
-            ext = np.full((2, 16), 0xA5, np.uint8)
+        for idle in (5000, 0):
+            assert lib.zp_parse_one_config(ctx, idle) == 0
+            for f in frames:
+                rec = np.zeros(1, zp.records.RECORD_DTYPE)
+                ext = np.full((2, 16), 0xA5, np.uint8)
+                buf = ctypes.create_string_buffer(f, max(len(f), 1))
+                rc = lib.zp_parse_one(ctx, ctypes.addressof(buf), len(f), rec.ctypes.data,
+                                      ext.ctypes.data)
+                err, wrec, wext = orc.parse_one(f)
+                assert rc == err and rec.tobytes() == orc.pack(wrec, wext).tobytes(), \
+                    (idle, len(f), rc, err)
+                assert ext.tobytes() == wext.view(np.uint8).tobytes(), (idle, len(f))
+    finally:
+        lib.zp_ctx_destroy(ctx)
+
+
+def test_parse_one_server_lifecycle(zp, golden):
+    """The resident zp_parse_one server across its life cycle: a tiny idle
+    timeout with random gaps between calls, so that the wave leaves between
+    requests, is relaunched by the next call, and sometimes leaves just as a
+    doorbell is rung (the host's stream check then relaunches it); stops and
+    mode switches in between. Every answer equals the oracle's on accepted
+    and rejected frames of every stack (c5, c4, c3, golden, mutated)."""
+    import ctypes
+    import time
+    rng = np.random.default_rng(29)
+    frames = [bytes.fromhex(fx["bytes"]) for fx in golden["fixtures"]]
+    for cfg, n in (("c5", 300), ("c4", 150), ("c3", 100)):
+        a, o, l_ = zp.batch.generate_host(cfg, n, first=5)
+        frames += [a[int(x):int(x) + int(y)].tobytes() for x, y in zip(o, l_)]
+    mut = []
+    for f in frames[:400]:
+        b = bytearray(f)
+        for _ in range(int(rng.integers(1, 3))):
+            b[int(rng.integers(0, min(len(b), 96)))] ^= 1 << int(rng.integers(0, 8))
+        mut.append(bytes(b))
+    frames += mut
+    want = [orc.parse_one(f) for f in frames]
+    assert sum(1 for w in want if w[0]) > 100 and sum(1 for w in want if not w[0]) > 400
+    lib = zp._lib.hip()
+    ctx = lib.zp_ctx_create(0, 0)
+    rec = np.zeros(1, zp.records.RECORD_DTYPE)
+    ext = np.zeros((2, 16), np.uint8)
+    try:
+        order = rng.permutation(len(frames))
+        for k, i in enumerate(order):
+            if k % 250 == 0:                              # mode switches / stops
+                lib.zp_parse_one_config(ctx, [40, 0, 2000, 40][(k // 250) % 4])
+            f = frames[i]
             buf = ctypes.create_string_buffer(f, max(len(f), 1))
             rc = lib.zp_parse_one(ctx, ctypes.addressof(buf), len(f), rec.ctypes.data,
                                   ext.ctypes.data)
-            err, wrec, wext = orc.parse_one(f)
-            assert rc == err and rec.tobytes() == orc.pack(wrec, wext).tobytes(), (len(f), rc, err)
-            assert ext.tobytes() == wext.view(np.uint8).tobytes(), len(f)
+            err, wrec, wext = want[i]
+            assert rc == err and rec.tobytes() == orc.pack(wrec, wext).tobytes(), (k, int(i), rc)
+            assert ext.tobytes() == wext.view(np.uint8).tobytes(), (k, int(i))
+            gap = rng.choice([0.0, 0.0, 20e-6, 45e-6, 200e-6])   # around the 40-us timeout
+            if gap:
+                time.sleep(gap)
     finally:
         lib.zp_ctx_destroy(ctx)

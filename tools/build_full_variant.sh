@@ -1,0 +1,17 @@
+#!/bin/bash
+# A whole libzp_hip.so built with extra flags (A/B of host + device code,
+# e.g. tools/parse_one_latency.py --lib tools/variants/<name>):
+#   tools/build_full_variant.sh <name> [flags...]
+cd "$(dirname "$0")/.." || exit 1
+name=$1; shift
+C=zero-packet_amd/csrc
+O=tools/variants/$name
+mkdir -p "$O"
+objs=()
+for f in zp_parse zp_ctx zp_gen zp_fields zp_ring zp_build zp_stats; do
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC "$@" -c $C/$f.hip -o "$O/$f.o" || exit 1
+  objs+=("$O/$f.o")
+done
+gcc -O3 -std=c11 -fPIC -c $C/zp_readers.c -o "$O/zp_readers.o" || exit 1
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$O/libzp_hip.so" "${objs[@]}" "$O/zp_readers.o" || exit 1
+rm -f "$O"/*.o

@@ -34,10 +34,18 @@ def main():
     ap.add_argument("--configs", default="c3,c5")
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--lib", default="", help="comma list of tools/variants/<name> builds whose "
+                    "fused kernel is timed too (fused_<name>)")
     a = ap.parse_args()
     zp = importlib.import_module("zero-packet_amd")
     C = zp.columns
     lib = zp._lib.hip()
+    vlibs = []
+    for v in [x for x in a.lib.split(",") if x]:
+        l = ctypes.CDLL(os.path.join(ROOT, "tools", "variants", v, "libzp_hip.so"))
+        l.zp_parse_batch_columns_device.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_uint64] + \
+            [ctypes.c_void_p] * 4
+        vlibs.append((v, l))
     d = torch.device("cuda:0")
     s = torch.cuda.current_stream(d)
     for cfg in a.configs.split(","):
@@ -64,10 +72,15 @@ def main():
                 return rc or lib.zp_extract_columns_device(
                     arena.data_ptr(), offs.data_ptr(), lens.data_ptr(), rec.data_ptr(), n, ptrs,
                     ctypes.c_void_p(s.cuda_stream))
-            res = {"fused": [], "split": []}
+            variants = [("fused", fused), ("split", split)]
+            for v, l in vlibs:
+                variants.append((f"fused_{v}", lambda l=l: l.zp_parse_batch_columns_device(
+                    arena.data_ptr(), offs.data_ptr(), lens.data_ptr(), n, rec.data_ptr(),
+                    ext.data_ptr(), ptrs, ctypes.c_void_p(s.cuda_stream))))
+            res = {v: [] for v, _ in variants}
             ref = None
             for r in range(a.rounds):
-                for v, fn in (("fused", fused), ("split", split)):
+                for v, fn in variants:
                     assert fn() == 0
                     ev = [(torch.cuda.Event(enable_timing=True),
                            torch.cuda.Event(enable_timing=True)) for _ in range(a.reps)]
@@ -81,8 +94,10 @@ def main():
                     elif not torch.equal(ref, got):
                         print(f"  !! {cfg} {label} {v}: results differ", flush=True)
             f, sp = (float(np.median(res[v])) for v in ("fused", "split"))
+            extra = "".join(f"  {v} {float(np.median(res[v])):7.3f} ms ({float(np.median(res[v])) / sp:5.3f})"
+                            for v, _ in variants[2:])
             print(f"{cfg} {label:18s} {width:3d} B/frame: fused {f:7.3f} ms  split {sp:7.3f} ms  "
-                  f"fused/split {f / sp:5.3f}", flush=True)
+                  f"fused/split {f / sp:5.3f}{extra}", flush=True)
             del out
         del arena, offs, lens, rec, ext
         torch.cuda.empty_cache()

@@ -1,7 +1,9 @@
 // Per-frame latency of zp_parse_one (PacketParser::parse for one frame,
 // parser.rs:53, through the GPU: H2D -> kernel -> D2H -> sync), the drop-in
 // for a caller that parses frame by frame. stdin: frame hex lines.
-//   parse_one_main <threads> <calls per thread>
+//   parse_one_main <threads> <calls per thread> [idle_us]
+// idle_us: zp_parse_one's mode (zp_parse_one_config): > 0 the resident server
+// wave with that idle timeout (default 5000), 0 one kernel launch per call.
 // Each thread owns one zp::Context (a zp_ctx may not be shared) and parses
 // the frames round robin; prints mean / p50 / p99 microseconds per call and
 // the aggregate calls per second.
@@ -15,9 +17,13 @@
 
 #include "zero_packet.hpp"
 
+// diagnostic builds (-DZP_ONE_STAMPS) export the server's in-kernel stamps
+extern "C" void zp__one_stamps(zp_ctx*, uint64_t*) __attribute__((weak));
+
 int main(int argc, char** argv) {
     const int threads = argc > 1 ? std::atoi(argv[1]) : 1;
     const int calls = argc > 2 ? std::atoi(argv[2]) : 2000;
+    const uint32_t idle_us = argc > 3 ? (uint32_t)std::atoi(argv[3]) : 5000u;
     std::vector<std::vector<uint8_t>> frames;
     std::string line;
     while (std::getline(std::cin, line)) {
@@ -28,8 +34,10 @@ int main(int argc, char** argv) {
     std::vector<std::vector<double>> lat(threads);
     std::vector<int> bad(threads, 0);
     std::vector<double> busy(threads, 0);
+    std::vector<std::vector<double>> st(4);    // thread 0: bell->tile, tile->stores done, polls
     auto worker = [&](int t) {
         zp::Context ctx(0);
+        ctx.parse_one_mode(idle_us);
         for (int w = 0; w < 50; ++w) ctx.parse(zp::Bytes{frames[0].data(), frames[0].size()});
         lat[t].reserve(calls);
         const auto tb = std::chrono::steady_clock::now();
@@ -39,6 +47,14 @@ int main(int argc, char** argv) {
             zp::PacketParser p = ctx.parse(zp::Bytes{f.data(), f.size()});
             const auto t1 = std::chrono::steady_clock::now();
             if (!p.ethernet) ++bad[t];
+            if (t == 0 && zp__one_stamps && idle_us) {
+                uint64_t s4[5];
+                zp__one_stamps(ctx.get(), s4);
+                st[0].push_back((s4[1] - s4[0]) / 100.0);
+                st[1].push_back((s4[2] - s4[1]) / 100.0);
+                st[2].push_back((double)s4[3]);
+                st[3].push_back((double)s4[4] / ((s4[1] - s4[0]) / 100.0));   // cycles per us
+            }
             lat[t].push_back(std::chrono::duration<double, std::micro>(t1 - t0).count());
         }
         busy[t] = std::chrono::duration<double>(std::chrono::steady_clock::now() - tb).count();
@@ -55,9 +71,15 @@ int main(int argc, char** argv) {
     for (double x : all) sum += x;
     int nbad = 0;
     for (int b : bad) nbad += b;
-    std::printf("{\"threads\": %d, \"calls\": %zu, \"mean_us\": %.2f, \"p50_us\": %.2f, "
+    std::printf("{\"idle_us\": %u, \"threads\": %d, \"calls\": %zu, \"mean_us\": %.2f, \"p50_us\": %.2f, "
                 "\"p99_us\": %.2f, \"calls_per_s\": %.0f, \"rejected\": %d}\n",
-                threads, all.size(), sum / all.size(), all[all.size() / 2],
+                idle_us, threads, all.size(), sum / all.size(), all[all.size() / 2],
                 all[(size_t)(all.size() * 0.99)], all.size() / wall, nbad);
+    if (!st[0].empty()) {
+        for (auto& v : st) std::sort(v.begin(), v.end());
+        std::printf("{\"server_stamps_p50\": {\"bell_to_tile_us\": %.2f, \"tile_to_stores_done_us\": %.2f, "
+                    "\"polls\": %.0f, \"shader_mhz\": %.0f}}\n", st[0][st[0].size() / 2],
+                    st[1][st[1].size() / 2], st[2][st[2].size() / 2], st[3][st[3].size() / 2]);
+    }
     return nbad ? 1 : 0;
 }

@@ -18,6 +18,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--calls", type=int, default=3000)
     ap.add_argument("--threads", default="1,8")
+    ap.add_argument("--modes", default="5000,0",
+                    help="zp_parse_one_config idle_us per run: >0 resident server, 0 launch per call")
     ap.add_argument("--lib", default="", help="directory of another libzp_hip.so build (A/B)")
     args = ap.parse_args()
     zp = importlib.import_module("zero-packet_amd")
@@ -28,12 +30,13 @@ def main():
     subprocess.run(["g++", "-std=c++17", "-O2", "-pthread", "-I", os.path.join(ROOT, "include"),
                     "-o", exe, os.path.join(ROOT, "tools", "latency", "parse_one_main.cpp"),
                     "-L" + lib, "-lzp_hip", "-Wl,-rpath," + lib], check=True)
-    for t in args.threads.split(","):
-        r = subprocess.run([exe, t, str(args.calls)], input=frames, capture_output=True, text=True,
-                           timeout=300)
-        print(r.stdout.strip() or r.stderr[-2000:], flush=True)
-        if r.returncode:
-            sys.exit(r.returncode)
+    for m in args.modes.split(","):
+        for t in args.threads.split(","):
+            r = subprocess.run([exe, t, str(args.calls), m], input=frames, capture_output=True,
+                               text=True, timeout=300)
+            print(r.stdout.strip() or r.stderr[-2000:], flush=True)
+            if r.returncode:
+                sys.exit(r.returncode)
 
 
 if __name__ == "__main__":

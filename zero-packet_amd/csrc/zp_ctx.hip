@@ -16,6 +16,7 @@
 #include <string.h>
 
 #include <pthread.h>
+#include <time.h>
 
 #include "../../include/zero_packet.h"
 
@@ -49,21 +50,44 @@ struct zp_ctx {
     uint32_t* d_bstart;
     zp_build_result* d_bres;
     uint32_t* h_bstart;
-    // zp_parse_one: one mapped, coherent pinned block (descriptors, record,
-    // ext entries, frame) the kernel reads and writes in place
+    // zp_parse_one: one mapped, coherent pinned block (doorbell, descriptors,
+    // record, ext entries, frame) the kernel reads and writes in place
     uint8_t* one_h;
     uint8_t* one_d;
     bool one_failed;              // the mapped block could not be allocated: batch path
+    // ... and its resident server wave (zp_one_server_kernel, zp_parse.hip)
+    uint32_t one_idle_us;         // server idle timeout; 0: one batch launch per call
+    uint64_t one_clock_khz;       // the device's constant clock (s_memrealtime)
+    uint32_t one_seq;             // last request the server finished
+    hipStream_t srv;              // the server's stream
+    bool srv_live;                // a server was launched and may still run
+    int64_t srv_seen_ns;          // host clock when the server last showed activity
 };
 
-// zp_parse_one's block: the frame at ONE_FRAME, its descriptor in front, the
-// outputs between them. Frames longer than ONE_MAX take the batch path.
-#define ONE_OFFS 0       // uint64_t: ONE_FRAME
-#define ONE_LENS 8       // uint32_t
-#define ONE_REC 16       // zp_record (8 B)
-#define ONE_EXT 32       // zp_ext_offsets[2]
-#define ONE_FRAME 64
+// zp_parse_one's block: the frame at ONE_FRAME, the doorbell and the batch
+// kernel's descriptor in front, the outputs between them (the server's
+// offsets are ZP_ONE_* in zp_parse.hip). Frames longer than ONE_MAX take the
+// batch path.
+#define ONE_BELL 0       // uint64_t: seq << 32 | length (server mode)
+#define ONE_OFFS 8       // uint64_t: ONE_FRAME (launch mode)
+#define ONE_LENS 16      // uint32_t (launch mode)
+#define ONE_REC 64       // zp_record (8 B)
+#define ONE_ACK 80       // uint32_t: seq of the last finished request (server mode)
+#define ONE_EXT 96       // zp_ext_offsets[2]
+#define ONE_FRAME 128
 #define ONE_MAX (64u << 10)
+#define ONE_STOP 0xFFFFFFFFu          // doorbell length: the server leaves
+#define ONE_IDLE_US_DEFAULT 5000u     // server idle timeout
+#define ONE_MARGIN_NS 500000          // host/device clock slack when judging the server alive
+
+extern "C" int zp__one_server_launch(uint8_t* blk_d, uint32_t seq, uint64_t idle_ticks,
+                                     void* stream);
+
+static int64_t mono_ns() {
+    timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (int64_t)t.tv_sec * 1000000000 + t.tv_nsec;
+}
 
 // Grows a device buffer to at least `need` elements (contents not kept).
 template <typename T>
@@ -89,11 +113,25 @@ static hipError_t grow(T** p, uint64_t* cap, uint64_t need) {
         }                                                                          \
     } while (0)
 
+// Stops the context's zp_parse_one server (if one may run) and waits for it.
+static void one_server_stop(zp_ctx* c) {
+    if (!c->srv_live) return;
+    const uint64_t bell = ((uint64_t)(c->one_seq + 1u) << 32) | ONE_STOP;
+    __atomic_store_n((uint64_t*)(c->one_h + ONE_BELL), bell, __ATOMIC_RELEASE);
+    (void)hipStreamSynchronize(c->srv);
+    // a server that had already left never saw the stop: the doorbell keeps
+    // seq + 1, so the next launch starts from there
+    c->one_seq += 1u;
+    c->srv_live = false;
+}
+
 extern "C" void zp_ctx_destroy(zp_ctx* c) {
     if (!c) return;
     int prev = 0;
     (void)hipGetDevice(&prev);
     (void)hipSetDevice(c->device);
+    one_server_stop(c);
+    if (c->srv) (void)hipStreamDestroy(c->srv);
     for (int k = 0; k < SLOTS; ++k) {
         if (c->s[k]) (void)hipStreamSynchronize(c->s[k]);
         (void)hipFree(c->d_arena[k]); (void)hipFree(c->d_offs[k]); (void)hipFree(c->d_lens[k]);
@@ -117,6 +155,7 @@ extern "C" zp_ctx* zp_ctx_create(int device, uint64_t chunk_bytes) {
     if (chunk_bytes < 65536) chunk_bytes = 65536;
     c->device = device;
     c->chunk_bytes = chunk_bytes;
+    c->one_idle_us = ONE_IDLE_US_DEFAULT;
     c->chunk_pkts = chunk_bytes / 64 + 1;
     (void)hipGetDevice(&prev);
     TRY(hipSetDevice(device));
@@ -133,6 +172,12 @@ extern "C" zp_ctx* zp_ctx_create(int device, uint64_t chunk_bytes) {
         TRY(hipHostMalloc(&c->h_lens[k], c->chunk_pkts * sizeof(uint32_t), hipHostMallocDefault));
         TRY(hipHostMalloc(&c->h_rec[k], c->chunk_pkts * sizeof(zp_record), hipHostMallocDefault));
         TRY(hipHostMalloc(&c->h_ext[k], 2 * c->chunk_pkts * sizeof(zp_ext_offsets), hipHostMallocDefault));
+    }
+    TRY(hipStreamCreateWithFlags(&c->srv, hipStreamNonBlocking));
+    {
+        int khz = 0;
+        TRY(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device));
+        c->one_clock_khz = (uint64_t)(khz > 0 ? khz : 100000);
     }
     (void)hipSetDevice(prev);
     return c;
@@ -271,29 +316,95 @@ extern "C" int zp_parse_batch_host(zp_ctx* c, const uint8_t* arena, uint64_t are
     return parse_host(c, arena, arena_bytes, offs, lens, n, recs, ext, ext ? ext + n : NULL);
 }
 
+// The mapped block of zp_parse_one (allocated on first use). False: none.
+static bool one_block(zp_ctx* c) {
+    if (!c->one_h && !c->one_failed) {
+        hipError_t a = hipHostMalloc((void**)&c->one_h, ONE_FRAME + ONE_MAX + 64,
+                                     hipHostMallocMapped | hipHostMallocCoherent);
+        if (a == hipSuccess) a = hipHostGetDevicePointer((void**)&c->one_d, c->one_h, 0);
+        if (a != hipSuccess) {                      // no mapped block: the batch path
+            (void)hipGetLastError();
+            (void)hipHostFree(c->one_h);
+            c->one_h = c->one_d = NULL;
+            c->one_failed = true;                   // not retried on every call
+        } else {
+            memset(c->one_h, 0, ONE_FRAME);
+        }
+    }
+    return c->one_h != NULL;
+}
+
+// One request through the resident server: doorbell, then spin on the
+// acknowledgement. The server is (re)launched when it is not running; the
+// host's clock says when it surely still runs (less than its idle timeout
+// since it last acknowledged), otherwise the stream says whether it left.
+static int one_via_server(zp_ctx* c, uint32_t len) {
+    int64_t now = mono_ns();
+    const int64_t idle_ns = (int64_t)c->one_idle_us * 1000;
+    if (c->srv_live && now - c->srv_seen_ns >= idle_ns - ONE_MARGIN_NS) {
+        const hipError_t q = hipStreamQuery(c->srv);
+        if (q == hipSuccess) c->srv_live = false;          // it left
+        else if (q != hipErrorNotReady) {
+            snprintf(g_ctx_error, ERRBUF_LEN, "zp_parse_one server: %s", hipGetErrorString(q));
+            return -2;
+        }
+    }
+    const uint64_t ticks = (uint64_t)c->one_idle_us * c->one_clock_khz / 1000u;
+    if (!c->srv_live) {
+        const int rc = zp__one_server_launch(c->one_d, c->one_seq, ticks, c->srv);
+        if (rc) return rc;
+        c->srv_live = true;
+        c->srv_seen_ns = now;
+    }
+    const uint32_t seq = c->one_seq + 1u;
+    volatile uint32_t* ack = (volatile uint32_t*)(c->one_h + ONE_ACK);
+    __atomic_store_n((uint64_t*)(c->one_h + ONE_BELL), ((uint64_t)seq << 32) | len,
+                     __ATOMIC_RELEASE);
+    const int64_t t0 = now;
+    int64_t next_check = t0 + 200000;                        // 200 us
+    for (uint32_t spin = 1;; ++spin) {
+        if (__atomic_load_n(ack, __ATOMIC_ACQUIRE) == seq) break;
+        __builtin_ia32_pause();
+        if ((spin & 1023u) == 0) {
+            now = mono_ns();
+            if (now < next_check) continue;
+            // The server may have left just before the doorbell (its idle
+            // timeout): then its stream is done and the request still open.
+            const hipError_t q = hipStreamQuery(c->srv);
+            if (q == hipSuccess) {
+                if (__atomic_load_n(ack, __ATOMIC_ACQUIRE) == seq) break;
+                const int rc = zp__one_server_launch(c->one_d, c->one_seq, ticks, c->srv);
+                if (rc) return rc;
+            } else if (q != hipErrorNotReady) {
+                snprintf(g_ctx_error, ERRBUF_LEN, "zp_parse_one server: %s", hipGetErrorString(q));
+                c->srv_live = false;
+                return -2;
+            }
+            if (now - t0 > 10000000000ll) {                  // 10 s: give up
+                snprintf(g_ctx_error, ERRBUF_LEN, "zp_parse_one: no answer from the server");
+                return -2;
+            }
+            next_check = now + 200000;
+        }
+    }
+    c->one_seq = seq;
+    c->srv_seen_ns = mono_ns();
+    return 0;
+}
+
 // One frame, latency first: the frame is copied into the context's mapped
-// pinned block and the kernel reads it and writes the record and chains
-// there over the host link (no separate DMA copies), then the stream is
-// synchronised: a launch and a wait per call. Frames past ONE_MAX take the
-// chunked batch path.
+// pinned block, where the GPU reads it and writes the record and chains
+// back over the host link. By default a resident server wave does the parse
+// (no launch per call); with zp_parse_one_config(ctx, 0) each call launches
+// the batch kernel on the block and waits on the stream. Frames past ONE_MAX
+// take the chunked batch path.
 extern "C" int zp_parse_one(zp_ctx* c, const uint8_t* frame, uint64_t len,
                             zp_record* record, zp_ext_offsets* ext) {
     if (!c || !record || len > 0xFFFFFFFFull || (!frame && len)) return -1;
     int prev = 0;
     (void)hipGetDevice(&prev);
     if (hipSetDevice(c->device) != hipSuccess) return -2;
-    if (!c->one_h && !c->one_failed && len <= ONE_MAX) {
-        hipError_t a = hipHostMalloc((void**)&c->one_h, ONE_FRAME + ONE_MAX + 64,
-                                     hipHostMallocMapped | hipHostMallocCoherent);
-        if (a == hipSuccess) a = hipHostGetDevicePointer((void**)&c->one_d, c->one_h, 0);
-        if (a != hipSuccess) {                      // no mapped block: the batch path below
-            (void)hipGetLastError();
-            (void)hipHostFree(c->one_h);
-            c->one_h = c->one_d = NULL;
-            c->one_failed = true;                   // not retried on every call
-        }
-    }
-    if (len > ONE_MAX || !c->one_h) {
+    if (len > ONE_MAX || !one_block(c)) {
         (void)hipSetDevice(prev);
         uint64_t off = 0;
         uint32_t l = (uint32_t)len;
@@ -302,36 +413,62 @@ extern "C" int zp_parse_one(zp_ctx* c, const uint8_t* frame, uint64_t len,
         const int rc = zp_parse_batch_host(c, frame ? frame : empty, len, &off, &l, 1, record, ext);
         return rc ? rc : (int)zp_rec_err(*record);
     }
-    hipError_t e = hipSuccess;
-    {
-        uint8_t* h = c->one_h;
+    uint8_t* h = c->one_h;
+    if (len) memcpy(h + ONE_FRAME, frame, len);
+    int rc;
+    if (c->one_idle_us) {
+        rc = one_via_server(c, (uint32_t)len);
+    } else {
         const uint64_t at = ONE_FRAME;
         const uint32_t l = (uint32_t)len;
         memcpy(h + ONE_OFFS, &at, 8);
         memcpy(h + ONE_LENS, &l, 4);
-        if (len) memcpy(h + ONE_FRAME, frame, len);
-        const int rc = zp_parse_batch_device(c->one_d, (const uint64_t*)(c->one_d + ONE_OFFS),
-                                             (const uint32_t*)(c->one_d + ONE_LENS), 1,
-                                             (zp_record*)(c->one_d + ONE_REC),
-                                             (zp_ext_offsets*)(c->one_d + ONE_EXT), c->s[0]);
-        if (rc) { (void)hipSetDevice(prev); return rc; }
-        e = hipStreamSynchronize(c->s[0]);
+        rc = zp_parse_batch_device(c->one_d, (const uint64_t*)(c->one_d + ONE_OFFS),
+                                   (const uint32_t*)(c->one_d + ONE_LENS), 1,
+                                   (zp_record*)(c->one_d + ONE_REC),
+                                   (zp_ext_offsets*)(c->one_d + ONE_EXT), c->s[0]);
+        if (!rc) {
+            const hipError_t e = hipStreamSynchronize(c->s[0]);
+            if (e != hipSuccess) {
+                snprintf(g_ctx_error, ERRBUF_LEN, "zp_parse_one: %s", hipGetErrorString(e));
+                rc = -2;
+            }
+        }
     }
     (void)hipSetDevice(prev);
-    if (e != hipSuccess) {
-        snprintf(g_ctx_error, ERRBUF_LEN, "zp_parse_one: %s", hipGetErrorString(e));
-        return -2;
-    }
-    memcpy(record, c->one_h + ONE_REC, sizeof(zp_record));
+    if (rc) return rc;
+    memcpy(record, h + ONE_REC, sizeof(zp_record));
     if (ext) {
         // entries are defined only where the record flags them (zero_packet.h)
-        const zp_ext_offsets* x = (const zp_ext_offsets*)(c->one_h + ONE_EXT);
+        const zp_ext_offsets* x = (const zp_ext_offsets*)(h + ONE_EXT);
         memset(ext, 0, 2 * sizeof(zp_ext_offsets));
         if (zp_rec_chain_inline(*record)) zp_rec_chain(*record, &ext[0]);   // ABI v6
         else if (record->flags & ZP_F_EXT) ext[0] = x[0];
         if (record->flags & ZP_F_INNER_EXT) ext[1] = x[1];
     }
     return (int)zp_rec_err(*record);
+}
+
+#ifdef ZP_ONE_STAMPS   // diagnostic build only: the server's last stamps
+extern "C" void zp__one_stamps(zp_ctx* c, uint64_t* out) {
+    memcpy(out, c->one_h + 32, 32);
+    memcpy(out + 4, c->one_h + 24, 8);
+}
+#endif
+
+// zp_parse_one's mode: idle_us = 0 launches the batch kernel per call;
+// otherwise a resident server wave answers and leaves after idle_us without
+// a request. Stops a running server either way (so this also quiesces the
+// context before a device-wide synchronisation).
+extern "C" int zp_parse_one_config(zp_ctx* c, uint32_t idle_us) {
+    if (!c) return -1;
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    if (hipSetDevice(c->device) != hipSuccess) return -2;
+    one_server_stop(c);
+    c->one_idle_us = idle_us;
+    (void)hipSetDevice(prev);
+    return 0;
 }
 
 // Several devices at once (one context each): the batch is cut into

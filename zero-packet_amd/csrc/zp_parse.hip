@@ -158,6 +158,7 @@ struct FrameView {
     uint32_t len;            // frame length
     uint4 xc;                // past the window: one cached 16-B chunk ...
     uint32_t xi;             // ... and its index from A & ~15 (~0: none)
+    bool sys;                // frame in host memory rewritten under the kernel: system-scope loads
 #ifdef ZP_FB2
     uint4 xc2;               // A/B: and the chunk after it
 #endif
@@ -207,7 +208,8 @@ __device__ __forceinline__ uint4 fb_chunk(FrameView& f, uint32_t c) {
 #ifdef ZP_DBG_FBCOUNT
         atomicAdd(&zp_fb_count, 1ull);
 #endif
-        f.xc = ldg16(((uintptr_t)f.g & ~(uintptr_t)15) + 16u * c);
+        const uintptr_t a = ((uintptr_t)f.g & ~(uintptr_t)15) + 16u * c;
+        f.xc = f.sys ? ld_sys16(a) : ldg16(a);
         f.xi = c;
     }
     return f.xc;
@@ -891,7 +893,7 @@ __device__ __forceinline__ void store_ext(zp_ext_offsets* base, uint64_t i, uint
 
 // Header walk + checksum verdict + record store of a streamed tile; with COLS
 // also the column views, from the same LDS window (no second pass).
-template <bool COLS>
+template <bool COLS, bool SYS = false>
 __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, WaveLds& lds,
                                             zp_record* __restrict__ records,
                                             zp_ext_offsets* __restrict__ ext,
@@ -910,6 +912,7 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
     fv.wlen = s.wlen;
     fv.xc = make_uint4(0, 0, 0, 0);
     fv.xi = ~0u;
+    fv.sys = SYS;
 #if ZP_REGION
     // the frame's cells and last chunk to registers, then its window to the
     // lane's private region (it overlays the cells and part of the tails)
@@ -1018,7 +1021,12 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
         const zp_u32x2 q = zp_pack(rec);
         __builtin_nontemporal_store(q.x ^ q.y, (uint32_t*)records + p);
 #else
-        __builtin_nontemporal_store(zp_pack(rec), (zp_u32x2*)(records + p));
+        if (SYS) {
+            const zp_u32x2 q = zp_pack(rec);
+            st_sys8(records + p, ((uint64_t)q.y << 32) | q.x);
+        } else {
+            __builtin_nontemporal_store(zp_pack(rec), (zp_u32x2*)(records + p));
+        }
 #endif
     }
     if (ext) {
@@ -1033,10 +1041,21 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
         const bool ho = (rec.flags & ZP_F_EXT) && !zp_chain_inline(rec),
                    hi = rec.flags & ZP_F_INNER_EXT;
         const uint64_t mo = __ballot(ho), mi = __ballot(hi);
+        if (SYS) {                                        // one frame: its own entries
+            if (ho) {
+                st_sys8(ext + p, ((uint64_t)w.outer.y << 32) | w.outer.x);
+                st_sys8((uint8_t*)(ext + p) + 8, ((uint64_t)w.outer.w << 32) | w.outer.z);
+            }
+            if (hi) {
+                st_sys8(ext + n + p, ((uint64_t)w.inner.y << 32) | w.inner.x);
+                st_sys8((uint8_t*)(ext + n + p) + 8, ((uint64_t)w.inner.w << 32) | w.inner.z);
+            }
+        } else {
         if (mo && (ho || __builtin_popcountll(mo) >= ZP_EXT_DENSE))
             store_ext(ext, p, ho ? w.outer : make_uint4(0, 0, 0, 0));
         if (mi && (hi || __builtin_popcountll(mi) >= ZP_EXT_DENSE))
             store_ext(ext, n + p, hi ? w.inner : make_uint4(0, 0, 0, 0));
+        }
     }
     if (COLS) {
         ViewReader rdr{fv};
@@ -1054,9 +1073,100 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
 #else
 #define ZP_KATTR __launch_bounds__(64 * ZP_WAVES)
 #endif
-// The fused parse + columns kernel carries the column getters too: no
-// waves-per-EU bound (at 96 VGPRs it spills).
+// The fused parse + columns kernel carries the column getters too.
+#ifdef ZP_COLS_WPE
+#define ZP_KATTR_COLS __launch_bounds__(64 * ZP_WAVES) __attribute__((amdgpu_waves_per_eu(ZP_COLS_WPE)))
+#else
 #define ZP_KATTR_COLS __launch_bounds__(64 * ZP_WAVES)
+#endif
+// One streamed tile: descriptors given (len, ga), stream, walk, verdict,
+// record store. Shared by the batch kernels and the resident zp_parse_one
+// server below.
+template <bool COLS, bool TINY = !COLS, bool SYS = false>
+__device__ __forceinline__ void parse_tile(uint64_t t, uint32_t len, uintptr_t ga, uint64_t n,
+                                           int lane, WaveLds& lds,
+                                           zp_record* __restrict__ records,
+                                           zp_ext_offsets* __restrict__ ext,
+                                           const ColPtrs& cols) {
+#ifdef ZP_STAMPS
+    const uint64_t wave_id = t;
+#endif
+    const uintptr_t fallback = (uintptr_t)&zp_safe_chunk;   // dummy loads when T == 0
+    uint4* win = &lds.win[0];
+    uint4* tail = &lds.win[ZP_WIN_CH * 64];
+#if ZP_TINY
+    // a tile of 64-B frames: registers only (wave-uniform test)
+    if (TINY && !__ballot(t * 64 + lane < n && len != 64u) &&
+        tiny_tile(t, len, ga, n, lane, records))
+        return;
+#endif
+    TileState s;
+    tile_setup(s, t, len, ga, n, lane, lds);
+    STAMP(1);
+    // stream: one group of ZP_G items per iteration (group 0 outside the
+    // loop, so no load is in flight across the loop back-edge)
+#if ZP_SMALL_G
+    if (s.nitems <= ZP_SMALL_G) {              // wave-uniform: a tile of small frames
+        // One group of ZP_SMALL_G items holds the whole tile (c2: 4 KiB):
+        // no dummy loads past the tile's end (c2 -8 %, c5 -1 %, c3/c4 0).
+        uint4 vs[ZP_SMALL_G];
+        uint32_t ks[ZP_SMALL_G];
+        issue_group<ZP_SMALL_G, false, SYS>(0, s.nitems, s.cur, s.R, lane, fallback, vs, ks);
+        STAMP(2);
+        consume_group<ZP_SMALL_G>(0, s.nitems, lane, vs, ks, win, tail, lds.cend, s.run);
+    } else
+#endif
+    {
+    uint4 va[ZP_G];
+    uint32_t ka[ZP_G];
+    issue_group<ZP_G, false, SYS>(0, s.nitems, s.cur, s.R, lane, fallback, va, ka);
+    STAMP(2);
+    consume_group<ZP_G>(0, s.nitems, lane, va, ka, win, tail, lds.cend, s.run);
+    for (uint32_t i0 = ZP_G; i0 < s.nitems; i0 += ZP_G) {
+#if ZP_TAIL_G2
+        if (s.nitems - i0 <= 2) {                 // the last 1-2 items as a pair
+            uint4 vt[2];
+            uint32_t kt[2];
+            issue_group<2, false, SYS>(i0, s.nitems, s.cur, s.R, lane, fallback, vt, kt);
+            consume_group<2>(i0, s.nitems, lane, vt, kt, win, tail, lds.cend, s.run);
+            break;
+        }
+#endif
+#if ZP_TAIL_G
+        // The last <= ZP_TAIL_G items as a small group: fewer dummy loads
+        // past the tile's end, whose address work (4 ds_bpermute each) and
+        // consume are not free (c5 -1.7 %, c6 -1.1 %, c3 -0.3 %, c4 0;
+        // profiles/r04_kbench_tail_group.log). Wave-uniform.
+        if (s.nitems - i0 <= ZP_TAIL_G) {
+            uint4 vt[ZP_TAIL_G];
+            uint32_t kt[ZP_TAIL_G];
+            issue_group<ZP_TAIL_G, false, SYS>(i0, s.nitems, s.cur, s.R, lane, fallback, vt, kt);
+            consume_group<ZP_TAIL_G>(i0, s.nitems, lane, vt, kt, win, tail, lds.cend, s.run);
+            break;
+        }
+#endif
+        issue_group<ZP_G, false, SYS>(i0, s.nitems, s.cur, s.R, lane, fallback, va, ka);
+        consume_group<ZP_G>(i0, s.nitems, lane, va, ka, win, tail, lds.cend, s.run);
+    }
+    }
+    wave_lds_fence();                          // LDS written by other lanes
+    // The frame address again, from its rank's stream origin (live
+    // through the stream anyway) instead of keeping it there: two VGPRs
+    // less at the stream's register peak. Only frames that own chunks
+    // (>= 64 B) ever use it.
+    {
+        const uint32_t r = s.rank & 63u;
+        const uintptr_t org = ((uintptr_t)bperm(s.R.org_hi, r) << 32) | bperm(s.R.org_lo, r);
+        s.ga = org + 16ull * bperm(s.R.pfx, r) + s.shift;
+    }
+#ifndef ZP_NO_PRIO
+    __builtin_amdgcn_s_setprio(0);             // walk at priority 0 ...
+#endif
+    STAMP(3);
+    tile_finish<COLS, SYS>(s, n, lane, lds, records, ext, cols);
+    STAMP(4);
+}
+
 template <bool COLS>
 __device__ __forceinline__ void parse_tiles(const uint8_t* __restrict__ arena,
                                             const uint64_t* __restrict__ offs,
@@ -1068,9 +1178,6 @@ __device__ __forceinline__ void parse_tiles(const uint8_t* __restrict__ arena,
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
     WaveLds& lds = lds_all[wid];
-    const uintptr_t fallback = (uintptr_t)&zp_safe_chunk;   // dummy loads when T == 0
-    uint4* win = &lds.win[0];
-    uint4* tail = &lds.win[ZP_WIN_CH * 64];
     // ZP_K consecutive tiles per wave (one contiguous band of the arena)
 #ifdef ZP_SEG
     // A/B: the grid's blocks interleaved over ZP_SEG contiguous segments of the
@@ -1101,77 +1208,7 @@ __device__ __forceinline__ void parse_tiles(const uint8_t* __restrict__ arena,
         uint32_t len;
         uintptr_t ga;
         load_desc(arena, offs, lens, n, t, lane, len, ga);
-#if ZP_TINY
-        // a tile of 64-B frames: registers only (wave-uniform test)
-        if (!COLS && !__ballot(t * 64 + lane < n && len != 64u) &&
-            tiny_tile(t, len, ga, n, lane, records))
-            continue;
-#endif
-        TileState s;
-        tile_setup(s, t, len, ga, n, lane, lds);
-        STAMP(1);
-        // stream: one group of ZP_G items per iteration (group 0 outside the
-        // loop, so no load is in flight across the loop back-edge)
-#if ZP_SMALL_G
-        if (s.nitems <= ZP_SMALL_G) {              // wave-uniform: a tile of small frames
-            // One group of ZP_SMALL_G items holds the whole tile (c2: 4 KiB):
-            // no dummy loads past the tile's end (c2 -8 %, c5 -1 %, c3/c4 0).
-            uint4 vs[ZP_SMALL_G];
-            uint32_t ks[ZP_SMALL_G];
-            issue_group<ZP_SMALL_G>(0, s.nitems, s.cur, s.R, lane, fallback, vs, ks);
-            STAMP(2);
-            consume_group<ZP_SMALL_G>(0, s.nitems, lane, vs, ks, win, tail, lds.cend, s.run);
-        } else
-#endif
-        {
-        uint4 va[ZP_G];
-        uint32_t ka[ZP_G];
-        issue_group<ZP_G>(0, s.nitems, s.cur, s.R, lane, fallback, va, ka);
-        STAMP(2);
-        consume_group<ZP_G>(0, s.nitems, lane, va, ka, win, tail, lds.cend, s.run);
-        for (uint32_t i0 = ZP_G; i0 < s.nitems; i0 += ZP_G) {
-#if ZP_TAIL_G2
-            if (s.nitems - i0 <= 2) {                 // the last 1-2 items as a pair
-                uint4 vt[2];
-                uint32_t kt[2];
-                issue_group<2>(i0, s.nitems, s.cur, s.R, lane, fallback, vt, kt);
-                consume_group<2>(i0, s.nitems, lane, vt, kt, win, tail, lds.cend, s.run);
-                break;
-            }
-#endif
-#if ZP_TAIL_G
-            // The last <= ZP_TAIL_G items as a small group: fewer dummy loads
-            // past the tile's end, whose address work (4 ds_bpermute each) and
-            // consume are not free (c5 -1.7 %, c6 -1.1 %, c3 -0.3 %, c4 0;
-            // profiles/r04_kbench_tail_group.log). Wave-uniform.
-            if (s.nitems - i0 <= ZP_TAIL_G) {
-                uint4 vt[ZP_TAIL_G];
-                uint32_t kt[ZP_TAIL_G];
-                issue_group<ZP_TAIL_G>(i0, s.nitems, s.cur, s.R, lane, fallback, vt, kt);
-                consume_group<ZP_TAIL_G>(i0, s.nitems, lane, vt, kt, win, tail, lds.cend, s.run);
-                break;
-            }
-#endif
-            issue_group<ZP_G>(i0, s.nitems, s.cur, s.R, lane, fallback, va, ka);
-            consume_group<ZP_G>(i0, s.nitems, lane, va, ka, win, tail, lds.cend, s.run);
-        }
-        }
-        wave_lds_fence();                          // LDS written by other lanes
-        // The frame address again, from its rank's stream origin (live
-        // through the stream anyway) instead of keeping it there: two VGPRs
-        // less at the stream's register peak. Only frames that own chunks
-        // (>= 64 B) ever use it.
-        {
-            const uint32_t r = s.rank & 63u;
-            const uintptr_t org = ((uintptr_t)bperm(s.R.org_hi, r) << 32) | bperm(s.R.org_lo, r);
-            s.ga = org + 16ull * bperm(s.R.pfx, r) + s.shift;
-        }
-#ifndef ZP_NO_PRIO
-        __builtin_amdgcn_s_setprio(0);             // walk at priority 0 ...
-#endif
-        STAMP(3);
-        tile_finish<COLS>(s, n, lane, lds, records, ext, cols);
-        STAMP(4);
+        parse_tile<COLS>(t, len, ga, n, lane, lds, records, ext, cols);
     }
 }
 
@@ -1235,5 +1272,115 @@ extern "C" int zp_parse_batch_columns_device(const uint8_t* arena, const uint64_
                        (hipStream_t)stream, arena, offs, lens, n, records, ext, c);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) { set_err("zp_parse_columns_kernel launch", e); return -2; }
+    return 0;
+}
+
+// --------------------------------------------------------------------------
+// zp_parse_one's resident server (zp_ctx.hip). PacketParser::parse for one
+// frame (parser.rs:53) costs a kernel launch and its completion signal when
+// each call launches the batch kernel (17.5 us). Instead one
+// wave per context stays resident and polls a doorbell in the context's
+// mapped host block: the host writes the frame, then the 64-bit doorbell
+// (sequence << 32 | length); the wave sees it, parses the frame in place as
+// a one-frame tile (parse_tile, the batch kernel's own code), writes the
+// record and the chains back into the block, and then the sequence number
+// into the acknowledgement word. The wave leaves when it has seen no
+// request for `idle` ticks of the 100 MHz constant clock (s_memrealtime) or
+// when the doorbell carries ZP_ONE_STOP, so it never spins past use; the
+// host relaunches it on the next call (zp_ctx.hip: the host knows from its
+// own clock whether the wave may have left, and from the stream whether it
+// did).
+// Memory order: the host block is fine-grained (coherent) host memory. The
+// doorbell, the frame bytes (stream and fallback loads) are read with
+// system-scope loads (sc0 sc1, past both caches), so a frame the host
+// rewrote since the last request is never served from a cache and no
+// cache-wide invalidate is needed; the record and chain stores are
+// system-scope (written through), and the wave waits for them to complete
+// before it stores the acknowledgement (guide: "sc0 sc1 stores and loads
+// both sides").
+// --------------------------------------------------------------------------
+#define ZP_ONE_BELL 0        // uint64_t: seq << 32 | frame length (host writes)
+#define ZP_ONE_REC 64        // zp_record (server writes)
+#define ZP_ONE_ACK 80        // uint32_t: seq of the last finished request (server writes)
+#define ZP_ONE_EXT 96        // zp_ext_offsets[2] (server writes)
+#define ZP_ONE_FRAME 128     // the frame (host writes)
+#define ZP_ONE_STOP 0xFFFFFFFFu   // doorbell length: leave now
+
+__global__ void __launch_bounds__(64)
+zp_one_server_kernel(uint8_t* blk, uint32_t seq, uint64_t idle) {
+    __shared__ WaveLds lds;
+    const int lane = threadIdx.x & 63;
+    const ColPtrs none{};
+    uint64_t last = __builtin_amdgcn_s_memrealtime();
+#ifdef ZP_ONE_STAMPS   // diagnostic build only (tools/parse_one_latency.py --lib)
+    uint64_t polls = 0;
+#endif
+    for (;;) {
+#ifdef ZP_ONE_STAMPS
+        ++polls;
+#endif
+        uint64_t bell = 0;
+        if (lane == 0)
+            bell = __hip_atomic_load((const uint64_t*)(blk + ZP_ONE_BELL), __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_SYSTEM);
+        const uint32_t bseq = (uint32_t)__builtin_amdgcn_readlane((uint32_t)(bell >> 32), 0);
+        const uint32_t blen = (uint32_t)__builtin_amdgcn_readlane((uint32_t)bell, 0);
+        if (bseq != seq) {                                   // wave-uniform
+            if (blen == ZP_ONE_STOP) break;
+#ifdef ZP_ONE_STAMPS
+            const uint64_t t_bell = __builtin_amdgcn_s_memrealtime();
+            const uint64_t c_bell = __builtin_amdgcn_s_memtime();
+#endif
+#ifdef ZP_ONE_ACQ   // A/B only: a cache-wide acquire (the loads are system-scope anyway)
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+#endif
+            __builtin_amdgcn_s_setprio(1);
+            // every load of the frame and every store of the results is
+            // system-scope (SYS): nothing is left in a cache to invalidate
+            // or write back
+            parse_tile<false, false, true>(0, blen, (uintptr_t)(blk + ZP_ONE_FRAME), 1, lane, lds,
+                                    (zp_record*)(blk + ZP_ONE_REC),
+                                    (zp_ext_offsets*)(blk + ZP_ONE_EXT), none);
+#ifdef ZP_ONE_REL   // A/B only: a cache-wide release
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+#endif
+#ifdef ZP_ONE_STAMPS
+            const uint64_t t_tile = __builtin_amdgcn_s_memrealtime();
+            const uint64_t c_tile = __builtin_amdgcn_s_memtime();
+#endif
+            // record + chains (system-scope stores) complete before the ack
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifdef ZP_ONE_STAMPS
+            if (lane == 0) {
+                st_sys8(blk + 32, t_bell);
+                st_sys8(blk + 40, t_tile);
+                st_sys8(blk + 48, __builtin_amdgcn_s_memrealtime());
+                st_sys8(blk + 56, polls);
+                st_sys8(blk + 24, c_tile - c_bell);
+            }
+            polls = 0;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+            if (lane == 0)
+                __hip_atomic_store((uint32_t*)(blk + ZP_ONE_ACK), bseq, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+            seq = bseq;
+            wave_lds_fence();                                 // LDS reused by the next request
+            last = __builtin_amdgcn_s_memrealtime();
+            continue;
+        }
+        if (__builtin_amdgcn_s_memrealtime() - last > idle) break;
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
+
+extern "C" __attribute__((visibility("hidden"))) int zp__one_server_launch(uint8_t* blk_d,
+                                                                            uint32_t seq,
+                                                                            uint64_t idle_ticks,
+                                                                            void* stream) {
+    hipLaunchKernelGGL(zp_one_server_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, blk_d,
+                       seq, idle_ticks);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) { set_err("zp_one_server_kernel launch", e); return -2; }
     return 0;
 }

@@ -38,6 +38,23 @@ __device__ __forceinline__ uint4 ld_stream(uintptr_t a) {
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+// System-scope 16-B load for frames in fine-grained host memory that the host
+// rewrites while the kernel runs (zp_parse_one's resident server): two
+// relaxed system-scope 8-B loads (sc0 sc1: past the vector L1 and the L2),
+// so no cache-wide invalidate is needed after the doorbell.
+__device__ __forceinline__ uint4 ld_sys16(uintptr_t a) {
+    const uint64_t x = __hip_atomic_load((const ZP_GLOBAL uint64_t*)a, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_SYSTEM);
+    const uint64_t y = __hip_atomic_load((const ZP_GLOBAL uint64_t*)(a + 8), __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_SYSTEM);
+    return make_uint4((uint32_t)x, (uint32_t)(x >> 32), (uint32_t)y, (uint32_t)(y >> 32));
+}
+// ... and the matching stores (write-through to the host, no L2 write-back
+// needed before the acknowledgement).
+__device__ __forceinline__ void st_sys8(void* p, uint64_t v) {
+    __hip_atomic_store((ZP_GLOBAL uint64_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // A readable 16-B chunk for masked lanes of frames that own no bytes.
 static __device__ uint4 zp_safe_chunk;
 
@@ -186,7 +203,7 @@ __device__ __forceinline__ void build_starts(uint32_t w0, const Cursor& c, const
 // Always issues exactly G loads (items past the end re-read the wave's last
 // chunk, or a dummy): a static load count keeps the compiler's s_waitcnt
 // exact.
-template <int G, bool T4 = false>
+template <int G, bool T4 = false, bool SYS = false>
 __device__ __forceinline__ void issue_group(uint32_t i0, uint32_t nitems, Cursor& c,
                                             const Ranked& R, int lane, uintptr_t fallback,
                                             uint4 (&v)[G], uint32_t (&keep)[G]) {
@@ -250,7 +267,7 @@ __device__ __forceinline__ void issue_group(uint32_t i0, uint32_t nitems, Cursor
     }
 #ifndef ZP_ABL_STREAM_OFF
 #pragma unroll
-    for (int q = 0; q < G; ++q) v[q] = ld_stream(a[q]);
+    for (int q = 0; q < G; ++q) v[q] = SYS ? ld_sys16(a[q]) : ld_stream(a[q]);
 #endif
     // Compiler barrier: keeps LLVM from sinking the loads below the consume
     // of the previous group (which would serialise the double buffer).

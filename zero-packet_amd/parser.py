@@ -19,6 +19,7 @@ unchecked view that from_record builds. internet_checksum,
 verify_internet_checksum and pseudo_header are checksum.rs:5,33,67 through
 the same library.
 """
+import atexit
 import ctypes
 import threading
 
@@ -590,4 +591,15 @@ def _default_ctx():
         _CTX = _lib.hip().zp_ctx_create(0, 0)
         if not _CTX:
             raise RuntimeError("zp_ctx_create failed: " + _lib.hip().zp_last_error().decode())
+        atexit.register(quiesce)
     return _CTX
+
+
+def quiesce():
+    """Stops the default context's resident zp_parse_one server wave now
+    (it also leaves by itself after 5 ms without a call; the next
+    PacketParser.parse relaunches it). Call before a device-wide
+    synchronisation to avoid waiting for that timeout."""
+    with _CTX_LOCK:
+        if _CTX is not None:
+            _lib.hip().zp_parse_one_config(_CTX, 5000)

@@ -1,8 +1,15 @@
-"""zp_record layout (include/zero_packet.h, ABI v5) as numpy dtypes."""
+"""zp_record layout (include/zero_packet.h, ABI v6) as numpy dtypes."""
+import ctypes
+
 import numpy as np
 
 # The 8-B record: flags (bits 0-23 ZP_F_*, 24-25 Ethernet code, 26-31 err)
-# and offs (bits 0-17 l4_off, 18-31 inner_off). unpack() gives the fields.
+# and offs (bits 0-17 l4_off, 18-31 inner_off when ZP_F_IP_IN_IP is set).
+# unpack() gives the fields.
+# Inline outer chain (ABI v6, ZP_CHAIN_INLINE): a frame without an ip_in_ip
+# header may carry its short RFC-ordered outer IPv6 extension chain in offs
+# bits 18-31 instead (bit 31 set, a 2-3-bit length code per header; no ext
+# entry is written): chain_inline() / inline_chains().
 # Far-L4 form (Ethernet code 3): offs is the whole L4 offset; the Ethernet
 # header length and inner_off are read from the frame (decode()).
 RECORD_DTYPE = np.dtype([("flags", "<u4"), ("offs", "<u4")])
@@ -108,7 +115,17 @@ def _ipv6_chain(frame, ip, chained, x):
     if not chained:
         return 0, frame[ip + 6]
     if x is None:
-        raise ValueError("the record flags an IPv6 extension chain: pass its ext entries")
+        # no entry given: the chain is walked again from the frame, as
+        # zp_rec_decode does (IPv6Reader::new's extension walk, ipv6.rs:159,
+        # through zp_reader_new)
+        from . import _lib
+        info = np.zeros(1, READER_INFO_DTYPE)
+        b = ctypes.create_string_buffer(frame[ip:], max(len(frame) - ip, 1))
+        rc = _lib.hip().zp_reader_new(READER_IPV6, ctypes.addressof(b), max(len(frame) - ip, 0),
+                                      info.ctypes.data)
+        if rc != 0 or not int(info[0]["flags"]) & F_EXT:
+            raise ValueError("the record flags an IPv6 extension chain the frame does not hold")
+        return int(info[0]["ext"]["len"]), int(info[0]["final_nh"])
     return int(x["len"]), int(x["final_nh"])
 
 
@@ -119,7 +136,8 @@ def decode(frame, rec, ext=None):
     Ethernet header length comes from the frame (ethernet.rs:155-179) and
     inner_off follows the outer IP header (IPv4 IHL * 4, ipv4.rs:228-258;
     IPv6 40 + extension_headers_len, ipv6.rs:283-285). ext: the frame's two
-    EXT_DTYPE entries, needed where the record flags a chain."""
+    EXT_DTYPE entries where the record flags a chain, or None: the chains are
+    then walked again from the frame (zp_reader_new), as in zp_rec_decode."""
     frame = bytes(frame)
     w, o = int(rec["flags"]), int(rec["offs"])
     out = dict(flags=0, err=w >> 26, eth_len=0, inner_off=0, l4_off=0, final_nh=0,
