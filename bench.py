@@ -29,6 +29,9 @@ Reported next to the GPU number:
                 a 2M-frame sample (zp_parse_batch_host), every rank at once,
                 frames summed over ranks / the slowest rank; never `value`;
                 rejected frames reported, not asserted
+  roofline.placement  a plain streaming read of the same arena (the
+                placement class: the parse's rate moves with the arena's
+                physical pages, DESIGN.md §4, and a pure read moves with it)
   config5       BASELINE config 5 in the same ranks after the headline: the
                 256M-frame IMIX stream (--c5-frames) cut into N contiguous
                 shards (strong scaling), its own timed loop of --steps
@@ -201,12 +204,41 @@ def pcie_inclusive(zp, arena, offs, lens, sample_pkts, barrier=lambda: None):
 PCIE_PATH = "pinned host -> H2D -> kernel -> D2H records, 2 streams x 256 MiB chunks"
 
 
+def placement_probe(zp, arena, kernel_ms, reps=5):
+    """The arena's placement class, measured: a plain streaming read of the
+    whole arena (zp_probe_read_device, HIP events on the launch stream) beside
+    the parse. Copies of one arena in different allocations parse at 0.77 /
+    0.80 / 0.82 of peak (the physical pages decide); a pure read
+    moves with them, so two lines of identical code on different placements
+    are told apart by read_gbs and parse_over_read."""
+    import ctypes
+    lib = zp._lib.hip()
+    sink = torch.zeros(1, dtype=torch.int32, device=arena.device)
+    stream = torch.cuda.current_stream(arena.device)
+    nb = arena.numel() // 16 * 16
+    s = ctypes.c_void_p(stream.cuda_stream)
+    zp._lib.check(lib.zp_probe_read_device(arena.data_ptr(), nb, sink.data_ptr(), s), "probe")
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(reps)]
+    for a, b in ev:
+        a.record(stream)
+        lib.zp_probe_read_device(arena.data_ptr(), nb, sink.data_ptr(), s)
+        b.record(stream)
+    torch.cuda.synchronize()
+    ms = float(np.median([a.elapsed_time(b) for a, b in ev]))
+    return {"arena_bytes": nb, "read_ms": round(ms, 4),
+            "read_gbs": round(nb / (ms * 1e-3) / 1e9, 1),
+            "parse_over_read": round(kernel_ms / ms, 4),
+            "arena_va_mod_1g": arena.data_ptr() % (1 << 30),
+            "probe": "zp_probe_read_device: grid-stride nt 16-B loads, 2048 x 256 lanes"}
+
+
 def gather_rows(row, world, rank, dev):
     """Every rank's float64 row as a [world, len(row)] numpy array (one
     all-reduce of a zero-padded table; no data-path collective)."""
     t = torch.zeros((world, len(row)), dtype=torch.float64, device=dev)
     t[rank] = torch.tensor(row, dtype=torch.float64)
-    if world > 1:
+    if dist.is_initialized():
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return t.cpu().numpy()
 
@@ -275,6 +307,9 @@ def main():
     ap.add_argument("--c5-frames", type=str, default=str(C5_TOTAL),
                     help="frames of the config-5 stream split over the ranks (e.g. 8M)")
     ap.add_argument("--no-c5", action="store_true", help="skip the config-5 leg")
+    ap.add_argument("--dist", action="store_true",
+                    help="initialise torch.distributed even at N = 1 (under a launcher): runs the "
+                         "RCCL init / barrier / all-reduce path of the multi-GPU line on one GPU")
     args = ap.parse_args()
 
     if args.gpus < 1:
@@ -297,14 +332,15 @@ def main():
     local_dev = local % ndev if shared else local
     torch.cuda.set_device(local_dev)
     dev = torch.device("cuda", local_dev)
-    if world > 1:
+    dist_on = world > 1 or (args.dist and "WORLD_SIZE" in os.environ)
+    if dist_on:
         if shared:
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=dev)
 
     def barrier():
-        if world > 1:
+        if dist_on:
             if shared:
                 dist.barrier()
             else:
@@ -353,7 +389,7 @@ def main():
     kms = [a.elapsed_time(b) for a, b in ev]
     t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if shared else dev)
     job_bytes = torch.tensor([total_bytes], dtype=torch.int64, device="cpu" if shared else dev)
-    if world > 1:
+    if dist_on:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dist.all_reduce(job_bytes, op=dist.ReduceOp.SUM)
     elapsed = float(t.item())
@@ -386,6 +422,7 @@ def main():
                      "algorithmic_bytes_per_launch": total_bytes},
     }
     coll_dev = "cpu" if shared else dev
+    out["roofline"]["placement"] = placement_probe(zp, arena, kmean)
     if not args.no_pcie:
         # every rank's host path at once: frames of all ranks / the slowest rank
         m, nb, sec, perr = pcie_inclusive(zp, arena, offs, lens, 1 << 21, barrier)
@@ -414,9 +451,11 @@ def main():
                                      world, rank, dev, barrier, coll_dev)
         # rejected frames are reported (rejected_per_rank), not asserted: the
         # generator writes valid frames, so a nonzero count is a finding
+    if dist_on:
+        out["config"]["dist_backend"] = dist.get_backend()
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 

@@ -414,6 +414,14 @@ uint32_t zp_pseudo_header(const uint8_t* src, const uint8_t* dest, uint32_t addr
  * Returns 0 or negative on launch failure. */
 int zp_stats_device(const zp_record* records, uint64_t n, uint64_t* counts, void* stream);
 
+/* Diagnostic: one plain streaming read of bytes [p, p + bytes) (device
+ * memory, 16-B aligned; the tail below 16 B is not read), enqueued on
+ * `stream`. bench.py times it over the arena beside the parse: the parse's
+ * rate moves with the physical placement of the arena and so
+ * does a pure read, which tells placements apart. sink: one device u32
+ * (practically never written). Returns 0 or negative. */
+int zp_probe_read_device(const uint8_t* p, uint64_t bytes, uint32_t* sink, void* stream);
+
 /* ------------------------------------------------------------------------- */
 /* Host-ring ingestion pipeline. Frames start in host */
 /* memory (a NIC ring / raw socket, README.md:85-115 of the reference). A     */

@@ -87,3 +87,26 @@ def test_bench_config5_and_host_path_over_ranks():
     h = r["h2d_d2h_inclusive"]
     assert h["ranks"] == 2 and h["sample_frames"] == 2 * (1 << 20) and h["gb_per_s"] > 0
     assert len(h["per_rank_gb_per_s"]) == 2
+
+
+def test_bench_rccl_path_one_rank():
+    """The RCCL branch of the multi-GPU line (init_process_group("nccl",
+    device_id=...), barrier(device_ids=...), the all-reduces of the timing
+    and of the per-rank rows) on one GPU: `torch.distributed.run
+    --nproc-per-node 1 bench.py --gpus 1 --dist` (a one-GPU box cannot start
+    two RCCL ranks; the 8-GPU node runs the same code with one rank per GPU)."""
+    n = 1 << 20
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.join(ROOT, "bench.py"), "--gpus", "1", "--dist", "--steps", "3",
+           "--warmup", "1", "--config", "c3", "--packets", str(n), "--c5-frames", "2M",
+           "--no-cpu"]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    r = json.loads(lines[0])
+    assert r["n_gpus"] == 1 and r["config"]["dist_backend"] == "nccl"
+    assert r["config5"]["rejected_per_rank"] == [0] and r["h2d_d2h_inclusive"]["ranks"] == 1
+    assert abs(r["value"] - n * 3 / (r["ms_per_step"] * 3 * 1e-3) / 1e6) < 0.02 * r["value"]

@@ -1,0 +1,66 @@
+"""The in-place builder's access pattern without its work (tools/membw.hip
+hdr_tiles): one wave per tile of 64 frames, the tile read once by 1 KiB
+nontemporal wave loads in groups of 8, then each lane writes back the whole
+64-B sectors covering its frame's first `hdr` bytes (the builder's header
+write-back). Store policies: plain / nt / write-through (agent-scope atomic
+stores) / none. Next to it: the parse kernel and the builder on 4M c3
+frames of the same box (tools/build_bench.py times the builder).
+
+    python tools/hdr_pattern.py [--hdr 54,108]
+"""
+import argparse
+import ctypes
+import importlib
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def timed(fn, reps=10):
+    s = torch.cuda.current_stream()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(reps)]
+    fn()
+    for a, b in ev:
+        a.record(s)
+        fn()
+        b.record(s)
+    torch.cuda.synchronize()
+    return float(np.median([a.elapsed_time(b) for a, b in ev]))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--hdr", default="54,108")
+    ap.add_argument("--region", type=int, default=50016, help="tile bytes (c3: 64 x 781.5 B)")
+    ap.add_argument("--gib", type=int, default=3, help="buffer (4M c3 frames = 3.28 GB)")
+    args = ap.parse_args()
+    mb = ctypes.CDLL(os.path.join(ROOT, "tools", "libmembw.so"))
+    mb.membw_hdr_tiles.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+                                   ctypes.c_uint32, ctypes.c_int, ctypes.c_uint32, ctypes.c_void_p]
+    d = torch.device("cuda:0")
+    buf = torch.randint(0, 255, (args.gib << 30,), dtype=torch.uint8, device=d)
+    nb = buf.numel() // args.region * args.region
+    for hdr in [int(x) for x in args.hdr.split(",")]:
+        for pol, name in ((3, "read only"), (1, "nt"), (0, "plain"), (2, "write-through")):
+            ms = timed(lambda: mb.membw_hdr_tiles(buf.data_ptr(), buf.numel(), args.region, hdr,
+                                                  pol, 13 * 1024, None))
+            print(f"hdr tiles region {args.region} hdr {hdr:4d} B {name:14s}: {ms:7.3f} ms "
+                  f"read {nb / ms / 1e6:6.0f} GB/s", flush=True)
+    zp = importlib.import_module("zero-packet_amd")
+    n = 1 << 22
+    arena, offs, lens = zp.batch.generate("c3", n, device=d)
+    rec = torch.empty((n, 8), dtype=torch.uint8, device=d)
+    lib = zp._lib.hip()
+    ms = timed(lambda: lib.zp_parse_batch_device(arena.data_ptr(), offs.data_ptr(), lens.data_ptr(),
+                                                 n, rec.data_ptr(), None, None))
+    print(f"parse 4M c3 frames ({int(lens.sum()) / 1e9:.2f} GB): {ms:.3f} ms", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -350,3 +350,81 @@ extern "C" int membw_copy_gap(const void* src, void* dst, uint64_t bytes, int ga
                        (const uint4*)src, (uint4*)dst, bytes / 16, (uint32_t)gap16);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+
+// The in-place builder's access pattern without its work:
+// read_tiles' stream over a tile of 64 frames of region/64 bytes each, then
+// every lane writes back the whole 64-B sectors covering bytes [f, f + hdr)
+// of its frame (f = its frame start: region/64 * lane, not 16-aligned), as
+// the builder's header write-back does. policy: 0 plain stores, 1
+// nontemporal, 2 write-through (sc1, system-coherent scope bit), 3 no write.
+template <int POLICY>
+__global__ void __launch_bounds__(64) hdr_tiles(uint8_t* __restrict__ p, uint64_t region,
+                                                uint32_t hdr, uint32_t lds_bytes) {
+    extern __shared__ uint32_t lds[];
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    const int lane = threadIdx.x;
+    const uint64_t w = blockIdx.x;
+    uint8_t* base = p + w * region;
+    const uint64_t nch = region / 16, items = (nch + 63) / 64;
+    uint32_t acc = 0;
+    for (uint64_t i = 0; i < items; i += 8) {
+        u32x4 v[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            uint64_t c = (i + q) * 64 + lane;
+            c = c < nch ? c : nch - 1;
+            v[q] = __builtin_nontemporal_load((const __attribute__((address_space(1))) u32x4*)(base + c * 16));
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc += v[q].x ^ v[q].y ^ v[q].z ^ v[q].w;
+    }
+    lds[lane] = acc;
+    __builtin_amdgcn_wave_barrier();
+    acc += lds[(lane + 1) & 63] + lds_bytes;
+    if (POLICY == 3) {
+        if (acc == 0x12345678u) base[0] = 1;
+        return;
+    }
+    const uint64_t f = (uint64_t)lane * (region / 64);
+    const uint64_t s0 = f & ~63ull, s1 = (f + hdr + 63) & ~63ull;
+    u32x4 val = {acc, acc ^ 1u, acc ^ 2u, acc ^ 3u};
+    for (uint64_t a = s0; a < s1 && a + 16 <= region; a += 16) {
+        __attribute__((address_space(1))) u32x4* q = (__attribute__((address_space(1))) u32x4*)(base + a);
+        if (POLICY == 0) *q = val;
+        else if (POLICY == 1) __builtin_nontemporal_store(val, q);
+        else __hip_atomic_store((__attribute__((address_space(1))) uint64_t*)q, ((uint64_t)val.y << 32) | val.x,
+                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+             __hip_atomic_store((__attribute__((address_space(1))) uint64_t*)q + 1, ((uint64_t)val.w << 32) | val.z,
+                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+extern "C" int membw_hdr_tiles(void* p, uint64_t bytes, uint64_t region, uint32_t hdr, int policy,
+                               uint32_t lds_bytes, void* stream) {
+    const uint64_t nreg = bytes / region;
+    hipStream_t s = (hipStream_t)stream;
+    uint8_t* q = (uint8_t*)p;
+    switch (policy) {
+    case 0: hipLaunchKernelGGL(hdr_tiles<0>, dim3((unsigned)nreg), dim3(64), lds_bytes, s, q, region, hdr, lds_bytes); break;
+    case 1: hipLaunchKernelGGL(hdr_tiles<1>, dim3((unsigned)nreg), dim3(64), lds_bytes, s, q, region, hdr, lds_bytes); break;
+    case 2: hipLaunchKernelGGL(hdr_tiles<2>, dim3((unsigned)nreg), dim3(64), lds_bytes, s, q, region, hdr, lds_bytes); break;
+    default: hipLaunchKernelGGL(hdr_tiles<3>, dim3((unsigned)nreg), dim3(64), lds_bytes, s, q, region, hdr, lds_bytes); break;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// Device buffers of a chosen allocation kind (record-store cost by the
+// records' memory type): 0 hipMalloc, 1 fine-grained, 2 uncached,
+// 3 contiguous. Returns NULL on failure.
+extern "C" void* membw_alloc(uint64_t bytes, int kind) {
+    void* p = nullptr;
+    hipError_t e;
+    switch (kind) {
+    case 0: e = hipMalloc(&p, bytes); break;
+    case 1: e = hipExtMallocWithFlags(&p, bytes, hipDeviceMallocFinegrained); break;
+    case 2: e = hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached); break;
+    default: e = hipExtMallocWithFlags(&p, bytes, hipDeviceMallocContiguous); break;
+    }
+    return e == hipSuccess ? p : nullptr;
+}
+extern "C" void membw_free(void* p) { (void)hipFree(p); }

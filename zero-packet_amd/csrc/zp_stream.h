@@ -89,9 +89,19 @@ __device__ __forceinline__ uint32_t chunk_sum(uint4 v, int l, int h, uint32_t s)
 // address of parity `odd`, with accumulator acc (fast path, exact V).
 __device__ __forceinline__ bool csum_ok(uint32_t acc, uint32_t V, bool odd) {
     if (acc == 0 && V == 0) return false;                  // S == 0 -> 0xFFFF
+#ifdef ZP_CSUM_FOLD
+    // A/B: 2^16 == 1 (mod 65535): t = acc + W folded by 16-bit limbs; t > 0,
+    // so t == 0 (mod 65535) iff the fold ends at 65535
+    const uint64_t t = (uint64_t)acc + (odd ? (uint64_t)V : (uint64_t)V << 8);
+    uint32_t x = (uint32_t)(t & 0xFFFFu) + (uint32_t)((t >> 16) & 0xFFFFu) + (uint32_t)(t >> 32);
+    x = (x & 0xFFFFu) + (x >> 16);
+    x = (x & 0xFFFFu) + (x >> 16);
+    return x == 65535u;
+#else
     uint32_t w = V % 65535u;
     if (!odd) w = (w * 256u) % 65535u;
     return ((acc % 65535u) + w) % 65535u == 0;
+#endif
 }
 
 // --------------------------------------------------------------------------
