@@ -252,8 +252,7 @@ def config5_leg(zp, total, steps, warmup, world, rank, dev, barrier, coll_dev):
     first, end = total * rank // world, total * (rank + 1) // world
     n = end - first
     arena, offs, lens = zp.batch.generate("c5", n, first=first, device=dev)
-    records = torch.empty((n, zp.records.RECORD_BYTES), dtype=torch.uint8, device=dev)
-    ext = torch.empty((2, n, 16), dtype=torch.uint8, device=dev)
+    records, ext = zp.batch.alloc_outputs(n, dev)
     nbytes = int(lens.to(torch.int64).sum().item())
     zp.batch.parse_batch(arena, offs, lens, records, ext, check=True)
     torch.cuda.synchronize()
@@ -356,8 +355,7 @@ def main():
         first, job_frames, scaling = rank * n, n * world, "weak"
     t0 = time.perf_counter()
     arena, offs, lens = zp.batch.generate(args.config, n, first=first, device=dev)
-    records = torch.empty((n, zp.records.RECORD_BYTES), dtype=torch.uint8, device=dev)
-    ext = torch.empty((2, n, 16), dtype=torch.uint8, device=dev)
+    records, ext = zp.batch.alloc_outputs(n, dev)
     torch.cuda.synchronize()
     total_bytes = int(lens.to(torch.int64).sum().item())
     log(f"[rank {rank}] generated {n} frames, {total_bytes/1e9:.2f} GB in "

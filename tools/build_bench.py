@@ -20,6 +20,8 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import ucmem  # noqa: E402
 
 
 def main():
@@ -38,6 +40,9 @@ def main():
                     help="every frame copies from blob offset 0 (L2-resident source; round 2)")
     ap.add_argument("--oracle-sample", type=int, default=2000,
                     help="frames compared byte for byte with the oracle builder")
+    ap.add_argument("--arena-mem", default="default", choices=["default", "uncached"],
+                    help="the frames' buffer in ordinary or uncached device memory (round 5: "
+                         "the header write-back's cost by memory kind)")
     ap.add_argument("--stamps", action="store_true",
                     help="phase shares from tools/variants/libzb_stamps.so (ZB_STAMPS build)")
     args = ap.parse_args()
@@ -48,6 +53,11 @@ def main():
     d = torch.device("cuda:0")
     n = args.frames
     arena, offs, lens = zp.batch.generate("c3", n, device=d)
+    if args.arena_mem == "uncached":
+        ua = ucmem.empty(arena.numel(), device=d)
+        ua.copy_(arena)
+        arena = ua
+        print("arena in uncached device memory", flush=True)
     ln = lens.cpu().numpy().astype(np.int64)
     rng = np.random.default_rng(7)
     ops = np.zeros(3 * n, B.OP_DTYPE)

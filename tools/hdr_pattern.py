@@ -19,6 +19,8 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import ucmem  # noqa: E402
 
 
 def timed(fn, reps=10):
@@ -39,12 +41,21 @@ def main():
     ap.add_argument("--hdr", default="54,108")
     ap.add_argument("--region", type=int, default=50016, help="tile bytes (c3: 64 x 781.5 B)")
     ap.add_argument("--gib", type=int, default=3, help="buffer (4M c3 frames = 3.28 GB)")
+    ap.add_argument("--uncached", action="store_true",
+                    help="the buffer in uncached device memory (tools/ucmem.py)")
     args = ap.parse_args()
     mb = ctypes.CDLL(os.path.join(ROOT, "tools", "libmembw.so"))
     mb.membw_hdr_tiles.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
                                    ctypes.c_uint32, ctypes.c_int, ctypes.c_uint32, ctypes.c_void_p]
     d = torch.device("cuda:0")
     buf = torch.randint(0, 255, (args.gib << 30,), dtype=torch.uint8, device=d)
+    if args.uncached:
+        zp = importlib.import_module("zero-packet_amd")
+        ub = ucmem.empty(buf.numel(), device=d)
+        ub.copy_(buf)
+        del buf
+        buf = ub
+        print("buffer in uncached device memory", flush=True)
     nb = buf.numel() // args.region * args.region
     for hdr in [int(x) for x in args.hdr.split(",")]:
         for pol, name in ((3, "read only"), (1, "nt"), (0, "plain"), (2, "write-through")):

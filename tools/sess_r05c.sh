@@ -6,3 +6,5 @@ timeout -k 10 200 python tools/hdr_pattern.py > gpurun_out/r05c_hdr_pattern.log 
 timeout -k 10 200 python tools/build_bench.py --oracle-sample 200 > gpurun_out/r05c_build_bench.log 2>&1 || exit $?
 timeout -k 10 300 python tools/rec_pattern.py > gpurun_out/r05c_rec_pattern.log 2>&1 || exit $?
 timeout -k 10 300 python tools/kbench.py --configs c5,c3,c4 --variants fold > gpurun_out/r05c_kb_fold.log 2>&1 || exit $?
+timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_parity.py -k "parse_one or golden" > gpurun_out/r05c_tests_po.log 2>&1 || exit $?
+timeout -k 10 300 python tools/parse_one_latency.py --calls 3000 > gpurun_out/r05c_lat.log 2>&1 || exit $?

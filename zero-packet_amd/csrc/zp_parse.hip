@@ -158,7 +158,7 @@ struct FrameView {
     uint32_t len;            // frame length
     uint4 xc;                // past the window: one cached 16-B chunk ...
     uint32_t xi;             // ... and its index from A & ~15 (~0: none)
-    bool sys;                // frame in host memory rewritten under the kernel: system-scope loads
+    uintptr_t sysbase;       // != 0: the frame lies in the host block at sysbase (system-scope loads)
 #ifdef ZP_FB2
     uint4 xc2;               // A/B: and the chunk after it
 #endif
@@ -209,7 +209,7 @@ __device__ __forceinline__ uint4 fb_chunk(FrameView& f, uint32_t c) {
         atomicAdd(&zp_fb_count, 1ull);
 #endif
         const uintptr_t a = ((uintptr_t)f.g & ~(uintptr_t)15) + 16u * c;
-        f.xc = f.sys ? ld_sys16(a) : ldg16(a);
+        f.xc = f.sysbase ? ld_sys16(f.sysbase, a) : ldg16(a);
         f.xi = c;
     }
     return f.xc;
@@ -897,7 +897,8 @@ template <bool COLS, bool SYS = false>
 __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, WaveLds& lds,
                                             zp_record* __restrict__ records,
                                             zp_ext_offsets* __restrict__ ext,
-                                            const ColPtrs& cols) {
+                                            const ColPtrs& cols, uintptr_t sysbase = 0,
+                                            zp_u32x2* rec_out = nullptr) {
     uint4* tail = &lds.win[ZP_WIN_CH * 64];
     const uint8_t* g = (const uint8_t*)s.ga;
 #ifdef ZP_STAMPS
@@ -912,7 +913,7 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
     fv.wlen = s.wlen;
     fv.xc = make_uint4(0, 0, 0, 0);
     fv.xi = ~0u;
-    fv.sys = SYS;
+    fv.sysbase = SYS ? sysbase : 0;
 #if ZP_REGION
     // the frame's cells and last chunk to registers, then its window to the
     // lane's private region (it overlays the cells and part of the tails)
@@ -1023,7 +1024,8 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
 #else
         if (SYS) {
             const zp_u32x2 q = zp_pack(rec);
-            st_sys8(records + p, ((uint64_t)q.y << 32) | q.x);
+            if (rec_out) *rec_out = q;                   // the caller stores it (with its ack)
+            else st_sys8(records + p, ((uint64_t)q.y << 32) | q.x);
         } else {
             __builtin_nontemporal_store(zp_pack(rec), (zp_u32x2*)(records + p));
         }
@@ -1087,7 +1089,8 @@ __device__ __forceinline__ void parse_tile(uint64_t t, uint32_t len, uintptr_t g
                                            int lane, WaveLds& lds,
                                            zp_record* __restrict__ records,
                                            zp_ext_offsets* __restrict__ ext,
-                                           const ColPtrs& cols) {
+                                           const ColPtrs& cols, uintptr_t sysbase = 0,
+                                           zp_u32x2* rec_out = nullptr) {
 #ifdef ZP_STAMPS
     const uint64_t wave_id = t;
 #endif
@@ -1111,7 +1114,7 @@ __device__ __forceinline__ void parse_tile(uint64_t t, uint32_t len, uintptr_t g
         // no dummy loads past the tile's end (c2 -8 %, c5 -1 %, c3/c4 0).
         uint4 vs[ZP_SMALL_G];
         uint32_t ks[ZP_SMALL_G];
-        issue_group<ZP_SMALL_G, false, SYS>(0, s.nitems, s.cur, s.R, lane, fallback, vs, ks);
+        issue_group<ZP_SMALL_G, false, SYS>(0, s.nitems, s.cur, s.R, lane, fallback, vs, ks, sysbase);
         STAMP(2);
         consume_group<ZP_SMALL_G>(0, s.nitems, lane, vs, ks, win, tail, lds.cend, s.run);
     } else
@@ -1119,7 +1122,7 @@ __device__ __forceinline__ void parse_tile(uint64_t t, uint32_t len, uintptr_t g
     {
     uint4 va[ZP_G];
     uint32_t ka[ZP_G];
-    issue_group<ZP_G, false, SYS>(0, s.nitems, s.cur, s.R, lane, fallback, va, ka);
+    issue_group<ZP_G, false, SYS>(0, s.nitems, s.cur, s.R, lane, fallback, va, ka, sysbase);
     STAMP(2);
     consume_group<ZP_G>(0, s.nitems, lane, va, ka, win, tail, lds.cend, s.run);
     for (uint32_t i0 = ZP_G; i0 < s.nitems; i0 += ZP_G) {
@@ -1127,7 +1130,7 @@ __device__ __forceinline__ void parse_tile(uint64_t t, uint32_t len, uintptr_t g
         if (s.nitems - i0 <= 2) {                 // the last 1-2 items as a pair
             uint4 vt[2];
             uint32_t kt[2];
-            issue_group<2, false, SYS>(i0, s.nitems, s.cur, s.R, lane, fallback, vt, kt);
+            issue_group<2, false, SYS>(i0, s.nitems, s.cur, s.R, lane, fallback, vt, kt, sysbase);
             consume_group<2>(i0, s.nitems, lane, vt, kt, win, tail, lds.cend, s.run);
             break;
         }
@@ -1140,12 +1143,12 @@ __device__ __forceinline__ void parse_tile(uint64_t t, uint32_t len, uintptr_t g
         if (s.nitems - i0 <= ZP_TAIL_G) {
             uint4 vt[ZP_TAIL_G];
             uint32_t kt[ZP_TAIL_G];
-            issue_group<ZP_TAIL_G, false, SYS>(i0, s.nitems, s.cur, s.R, lane, fallback, vt, kt);
+            issue_group<ZP_TAIL_G, false, SYS>(i0, s.nitems, s.cur, s.R, lane, fallback, vt, kt, sysbase);
             consume_group<ZP_TAIL_G>(i0, s.nitems, lane, vt, kt, win, tail, lds.cend, s.run);
             break;
         }
 #endif
-        issue_group<ZP_G, false, SYS>(i0, s.nitems, s.cur, s.R, lane, fallback, va, ka);
+        issue_group<ZP_G, false, SYS>(i0, s.nitems, s.cur, s.R, lane, fallback, va, ka, sysbase);
         consume_group<ZP_G>(i0, s.nitems, lane, va, ka, win, tail, lds.cend, s.run);
     }
     }
@@ -1163,7 +1166,7 @@ __device__ __forceinline__ void parse_tile(uint64_t t, uint32_t len, uintptr_t g
     __builtin_amdgcn_s_setprio(0);             // walk at priority 0 ...
 #endif
     STAMP(3);
-    tile_finish<COLS, SYS>(s, n, lane, lds, records, ext, cols);
+    tile_finish<COLS, SYS>(s, n, lane, lds, records, ext, cols, sysbase, rec_out);
     STAMP(4);
 }
 
@@ -1303,6 +1306,7 @@ extern "C" int zp_parse_batch_columns_device(const uint8_t* arena, const uint64_
 #define ZP_ONE_REC 64        // zp_record (server writes)
 #define ZP_ONE_ACK 80        // uint32_t: seq of the last finished request (server writes)
 #define ZP_ONE_EXT 96        // zp_ext_offsets[2] (server writes)
+#define ZP_ONE_ACK16_OFF 80  // ZP_ONE_ACK16 (A/B): {record, seq, check} in one 16-B store (over ZP_ONE_ACK)
 #define ZP_ONE_FRAME 128     // the frame (host writes)
 #define ZP_ONE_STOP 0xFFFFFFFFu   // doorbell length: leave now
 
@@ -1338,9 +1342,16 @@ zp_one_server_kernel(uint8_t* blk, uint32_t seq, uint64_t idle) {
             // every load of the frame and every store of the results is
             // system-scope (SYS): nothing is left in a cache to invalidate
             // or write back
+#ifdef ZP_ONE_ACK16
+            zp_u32x2 rq = {0u, 0u};
             parse_tile<false, false, true>(0, blen, (uintptr_t)(blk + ZP_ONE_FRAME), 1, lane, lds,
                                     (zp_record*)(blk + ZP_ONE_REC),
-                                    (zp_ext_offsets*)(blk + ZP_ONE_EXT), none);
+                                    (zp_ext_offsets*)(blk + ZP_ONE_EXT), none, (uintptr_t)blk, &rq);
+#else
+            parse_tile<false, false, true>(0, blen, (uintptr_t)(blk + ZP_ONE_FRAME), 1, lane, lds,
+                                    (zp_record*)(blk + ZP_ONE_REC),
+                                    (zp_ext_offsets*)(blk + ZP_ONE_EXT), none, (uintptr_t)blk);
+#endif
 #ifdef ZP_ONE_REL   // A/B only: a cache-wide release
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
 #endif
@@ -1348,8 +1359,43 @@ zp_one_server_kernel(uint8_t* blk, uint32_t seq, uint64_t idle) {
             const uint64_t t_tile = __builtin_amdgcn_s_memrealtime();
             const uint64_t c_tile = __builtin_amdgcn_s_memtime();
 #endif
+#ifdef ZP_ONE_TWICE   // diagnostic: the same tile again, warm (instruction cache, LDS)
+            {
+                wave_lds_fence();
+                const uint64_t t2 = __builtin_amdgcn_s_memrealtime();
+                parse_tile<false, false, true>(0, blen, (uintptr_t)(blk + ZP_ONE_FRAME), 1, lane, lds,
+                                        (zp_record*)(blk + ZP_ONE_REC),
+                                        (zp_ext_offsets*)(blk + ZP_ONE_EXT), none, (uintptr_t)blk);
+                // the second pass's ticks (bell_to_tile stays the first pass)
+                if (lane == 0) st_sys8(blk + 16, __builtin_amdgcn_s_memrealtime() - t2);
+            }
+#endif
+#ifdef ZP_ONE_ACK16
+            // The record and the ack leave in ONE 16-B system-scope store
+            // from lane 0 ({record, seq, check}; the host accepts it when the
+            // check matches), so only chain entries, when the record flags
+            // any, are waited for before it.
+            {
+                const uint32_t fl = __builtin_amdgcn_readlane(rq.x, 0);
+                const uint32_t of = __builtin_amdgcn_readlane(rq.y, 0);
+                // zp_rec_chain_inline (include/zero_packet.h): no entry written
+                const bool inl = ((fl >> 24) & 3u) != ZP_ETH_CODE_FAR &&
+                                 (fl & (ZP_F_EXT | ZP_F_IP_IN_IP)) == ZP_F_EXT &&
+                                 (of & ZP_CHAIN_INLINE) != 0;
+                const bool chains = (fl >> 26) == 0 &&
+                    ((fl & ZP_F_INNER_EXT) || ((fl & ZP_F_EXT) && !inl));
+                if (chains) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (lane == 0) {
+                    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+                        (void*)blk, (short)0, (int)ZP_SYS_BYTES, 0x00020000);
+                    const zp_u32x4 q = {fl, of, bseq, fl ^ of ^ bseq ^ 0xA5A5A5A5u};
+                    __builtin_amdgcn_raw_buffer_store_b128(q, r, ZP_ONE_ACK16_OFF, 0, 1 | 16);
+                }
+            }
+#else
             // record + chains (system-scope stores) complete before the ack
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
 #ifdef ZP_ONE_STAMPS
             if (lane == 0) {
                 st_sys8(blk + 32, t_bell);
@@ -1361,9 +1407,11 @@ zp_one_server_kernel(uint8_t* blk, uint32_t seq, uint64_t idle) {
             polls = 0;
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
+#ifndef ZP_ONE_ACK16
             if (lane == 0)
                 __hip_atomic_store((uint32_t*)(blk + ZP_ONE_ACK), bseq, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_SYSTEM);
+#endif
             seq = bseq;
             wave_lds_fence();                                 // LDS reused by the next request
             last = __builtin_amdgcn_s_memrealtime();

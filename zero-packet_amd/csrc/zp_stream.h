@@ -39,15 +39,18 @@ __device__ __forceinline__ uint4 ld_stream(uintptr_t a) {
 }
 
 // System-scope 16-B load for frames in fine-grained host memory that the host
-// rewrites while the kernel runs (zp_parse_one's resident server): two
-// relaxed system-scope 8-B loads (sc0 sc1: past the vector L1 and the L2),
-// so no cache-wide invalidate is needed after the doorbell.
-__device__ __forceinline__ uint4 ld_sys16(uintptr_t a) {
-    const uint64_t x = __hip_atomic_load((const ZP_GLOBAL uint64_t*)a, __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_SYSTEM);
-    const uint64_t y = __hip_atomic_load((const ZP_GLOBAL uint64_t*)(a + 8), __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_SYSTEM);
-    return make_uint4((uint32_t)x, (uint32_t)(x >> 32), (uint32_t)y, (uint32_t)(y >> 32));
+// rewrites while the kernel runs (zp_parse_one's resident server, whose block
+// of ZP_SYS_BYTES starts at `base`): one buffer load with sc0 sc1 (system
+// scope: past the vector L1 and the L2), so no cache-wide invalidate is
+// needed after the doorbell. Addresses outside the block (the dummy loads of
+// an empty tile) read 0 instead of faulting.
+#define ZP_SYS_BYTES (128u + (64u << 10) + 64u)   // = zp_ctx.hip's mapped block
+__device__ __forceinline__ uint4 ld_sys16(uintptr_t base, uintptr_t a) {
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)ZP_SYS_BYTES, 0x00020000);
+    const zp_u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(uint32_t)(a - base), 0,
+                                                              1 | 16);   // sc0 sc1
+    return make_uint4(v.x, v.y, v.z, v.w);
 }
 // ... and the matching stores (write-through to the host, no L2 write-back
 // needed before the acknowledgement).
@@ -216,7 +219,8 @@ __device__ __forceinline__ void build_starts(uint32_t w0, const Cursor& c, const
 template <int G, bool T4 = false, bool SYS = false>
 __device__ __forceinline__ void issue_group(uint32_t i0, uint32_t nitems, Cursor& c,
                                             const Ranked& R, int lane, uintptr_t fallback,
-                                            uint4 (&v)[G], uint32_t (&keep)[G]) {
+                                            uint4 (&v)[G], uint32_t (&keep)[G],
+                                            uintptr_t sysbase = 0) {
     uintptr_t a[G];
 #ifndef ZP_FMASK_ITEM
     // The G items' frame-start masks in one LDS round trip (G divides 64, so
@@ -277,7 +281,15 @@ __device__ __forceinline__ void issue_group(uint32_t i0, uint32_t nitems, Cursor
     }
 #ifndef ZP_ABL_STREAM_OFF
 #pragma unroll
-    for (int q = 0; q < G; ++q) v[q] = SYS ? ld_sys16(a[q]) : ld_stream(a[q]);
+    for (int q = 0; q < G; ++q) {
+        // SYS: lanes past the frame's end and items past the tile load
+        // nothing (an offset past the buffer reads 0 without a memory
+        // access): system-scope loads of one address from many lanes are not
+        // merged, and the clamped duplicates cost ~0.1 us each over the host
+        // link (a 1.5 KB frame took 22 us with them)
+        v[q] = SYS ? ld_sys16(sysbase, (keep[q] & KEEP_IN) ? a[q] : sysbase + 0xFFFFFFF0u)
+                   : ld_stream(a[q]);
+    }
 #endif
     // Compiler barrier: keeps LLVM from sinking the loads below the consume
     // of the previous group (which would serialise the double buffer).
