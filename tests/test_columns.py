@@ -169,12 +169,17 @@ def test_gpu_columns_vs_oracle(zp, golden, case):
             (g != want[name]).reshape(len(g), -1).any(1))[0][:5])
     for name in ("src_port", "dest_addr"):
         assert np.array_equal(sub[name].cpu().numpy(), want[name])
-    # the fused parse + columns pass gives the same records and columns
-    frecs, _, fcols = zp.columns.parse_with_columns(a, o, l_)
-    fsub = zp.columns.parse_with_columns(a, o, l_, names=["tcp_seq", "vlan_tci"])[2]
-    torch.cuda.synchronize()
-    assert torch.equal(frecs, recs)
-    for name in zp.columns.NAMES:
-        assert np.array_equal(fcols[name].cpu().numpy(), want[name]), ("fused", case, name)
-    for name in ("tcp_seq", "vlan_tci"):
-        assert np.array_equal(fsub[name].cpu().numpy(), want[name])
+    # parse_with_columns gives the same records and columns on every path:
+    # the fused pass, parse + extract, and "auto" while it times both (the
+    # first 4 calls of a workload) and after it has chosen
+    for mode in ["fused", "split"] + ["auto"] * 5:
+        frecs, _, fcols = zp.columns.parse_with_columns(a, o, l_, mode=mode)
+        fsub = zp.columns.parse_with_columns(a, o, l_, names=["tcp_seq", "vlan_tci"],
+                                             mode=mode)[2]
+        torch.cuda.synchronize()
+        assert torch.equal(frecs, recs), mode
+        for name in zp.columns.NAMES:
+            assert np.array_equal(fcols[name].cpu().numpy(), want[name]), (mode, case, name)
+        for name in ("tcp_seq", "vlan_tci"):
+            assert np.array_equal(fsub[name].cpu().numpy(), want[name]), mode
+    assert zp.columns.auto_choice(a, o.numel(), zp.columns.NAMES) in ("fused", "split")

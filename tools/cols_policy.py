@@ -72,7 +72,10 @@ def main():
                 return rc or lib.zp_extract_columns_device(
                     arena.data_ptr(), offs.data_ptr(), lens.data_ptr(), rec.data_ptr(), n, ptrs,
                     ctypes.c_void_p(s.cuda_stream))
-            variants = [("fused", fused), ("split", split)]
+            variants = [("fused", fused), ("split", split),
+                        ("auto", lambda: C.parse_with_columns(arena, offs, lens, names=names,
+                                                              records=rec, ext=ext, out=out,
+                                                              check=False) and 0)]
             for v, l in vlibs:
                 variants.append((f"fused_{v}", lambda l=l: l.zp_parse_batch_columns_device(
                     arena.data_ptr(), offs.data_ptr(), lens.data_ptr(), n, rec.data_ptr(),
@@ -81,7 +84,7 @@ def main():
             ref = None
             for r in range(a.rounds):
                 for v, fn in variants:
-                    assert fn() == 0
+                    assert not fn()
                     ev = [(torch.cuda.Event(enable_timing=True),
                            torch.cuda.Event(enable_timing=True)) for _ in range(a.reps)]
                     for x, y in ev:
@@ -96,6 +99,7 @@ def main():
             f, sp = (float(np.median(res[v])) for v in ("fused", "split"))
             extra = "".join(f"  {v} {float(np.median(res[v])):7.3f} ms ({float(np.median(res[v])) / sp:5.3f})"
                             for v, _ in variants[2:])
+            extra += f"  [auto chose {C.auto_choice(arena, n, names)}]"
             print(f"{cfg} {label:18s} {width:3d} B/frame: fused {f:7.3f} ms  split {sp:7.3f} ms  "
                   f"fused/split {f / sp:5.3f}{extra}", flush=True)
             del out

@@ -34,7 +34,7 @@ int main(int argc, char** argv) {
     std::vector<std::vector<double>> lat(threads);
     std::vector<int> bad(threads, 0);
     std::vector<double> busy(threads, 0);
-    std::vector<std::vector<double>> st(5);    // thread 0: bell->tile, tile->stores done, polls
+    std::vector<std::vector<double>> st(5), ph(8);    // thread 0: bell->tile, tile->stores done, polls
     auto worker = [&](int t) {
         zp::Context ctx(0);
         ctx.parse_one_mode(idle_us);
@@ -48,13 +48,15 @@ int main(int argc, char** argv) {
             const auto t1 = std::chrono::steady_clock::now();
             if (!p.ethernet) ++bad[t];
             if (t == 0 && zp__one_stamps && idle_us) {
-                uint64_t s4[6] = {0, 0, 0, 0, 0, 0};
+                uint64_t s4[14] = {0};
                 zp__one_stamps(ctx.get(), s4);
                 st[0].push_back((s4[1] - s4[0]) / 100.0);
                 st[1].push_back((s4[2] - s4[1]) / 100.0);
                 st[2].push_back((double)s4[3]);
                 st[3].push_back((double)s4[4] / ((s4[1] - s4[0]) / 100.0));   // cycles per us
                 st[4].push_back(s4[5] / 100.0);          // ZP_ONE_TWICE builds: the warm second pass
+                for (int k = 1; k < 8; ++k)            // phase k end - bell (us)
+                    ph[k].push_back(s4[6 + k] ? ((double)s4[6 + k] - (double)s4[0]) / 100.0 : -1.0);
             }
             lat[t].push_back(std::chrono::duration<double, std::micro>(t1 - t0).count());
         }
@@ -82,6 +84,12 @@ int main(int argc, char** argv) {
                     "\"polls\": %.0f, \"shader_mhz\": %.0f, \"second_pass_us\": %.2f}}\n",
                     st[0][st[0].size() / 2], st[1][st[1].size() / 2], st[2][st[2].size() / 2],
                     st[3][st[3].size() / 2], st[4][st[4].size() / 2]);
+        std::printf("{\"server_phase_end_after_bell_us_p50\": [");
+        for (int k = 1; k < 8; ++k) {
+            std::sort(ph[k].begin(), ph[k].end());
+            std::printf("%s%.2f", k > 1 ? ", " : "", ph[k][ph[k].size() / 2]);
+        }
+        std::printf("], \"phases\": \"1 setup, 2 first issue, 3 stream done, 4 tile done, 5 walk, 6 verdict, 7 -\"}\n");
     }
     return nbad ? 1 : 0;
 }

@@ -74,13 +74,40 @@ def extract(arena, offs, lens, records, names=None, out=None, stream=None, check
     return {k: out[k] for k in names}
 
 
+# Path choice of parse_with_columns(mode="auto") per workload key: the fused
+# kernel (one pass) wins on most traffic, but plain IPv4 frames with wide
+# column requests run faster as parse + extract (round 4/5: c3 with all 29
+# columns +2-3 % fused; c4/c5/c6 -11 to -23 %). The library
+# times both paths on the first calls of a workload and keeps the faster one.
+_AUTO_TRIALS = 2
+_auto = {}
+
+
+def _auto_key(arena, n, names):
+    return (arena.device.index, tuple(sorted(names)), max(n, 1).bit_length())
+
+
+def auto_choice(arena, n, names):
+    """The path parse_with_columns(mode="auto") uses for this workload key
+    (None while it is still timing both)."""
+    st = _auto.get(_auto_key(arena, n, names))
+    return st["choice"] if st else None
+
+
 def parse_with_columns(arena, offs, lens, names=None, records=None, ext=None, out=None,
-                       stream=None, check=True):
-    """zp_parse_batch_columns_device: records and the requested columns in one
-    pass over the frames. Returns (records, ext, {name: tensor})."""
+                       stream=None, check=True, mode="auto"):
+    """Records and the requested columns of every frame. Returns (records,
+    ext, {name: tensor}); the results are the same on every path.
+    mode: "fused" = zp_parse_batch_columns_device (one pass over the frames);
+    "split" = zp_parse_batch_device then zp_extract_columns_device on the same
+    stream; "auto" (default) = the faster of the two for this workload (device,
+    column set, batch-size octave), timed with HIP events on the launch stream
+    over the first 2 calls of each path (those calls synchronise), then kept."""
     for t in (arena, offs, lens):
         if not t.is_cuda:
             raise RuntimeError("columns.parse_with_columns needs device tensors (no CPU fallback)")
+    if mode not in ("auto", "fused", "split"):
+        raise ValueError(f"mode {mode!r}: auto, fused or split")
     n = offs.numel()
     d = arena.device
     records, ext = alloc_outputs(n, d, records, ext)
@@ -95,8 +122,39 @@ def parse_with_columns(arena, offs, lens, names=None, records=None, ext=None, ou
                 [(out[k], width(k)) for k in names], bounds=check)
     s = ctypes.c_void_p(stream) if stream is not None else \
         ctypes.c_void_p(torch.cuda.current_stream(d).cuda_stream)
-    rc = _lib.hip().zp_parse_batch_columns_device(arena.data_ptr(), offs.data_ptr(),
-                                                  lens.data_ptr(), n, records.data_ptr(),
-                                                  ext.data_ptr(), ptrs, s)
-    _lib.check(rc, "zp_parse_batch_columns_device")
+    lib = _lib.hip()
+
+    def fused():
+        _lib.check(lib.zp_parse_batch_columns_device(arena.data_ptr(), offs.data_ptr(),
+                                                     lens.data_ptr(), n, records.data_ptr(),
+                                                     ext.data_ptr(), ptrs, s),
+                   "zp_parse_batch_columns_device")
+
+    def split():
+        _lib.check(lib.zp_parse_batch_device(arena.data_ptr(), offs.data_ptr(), lens.data_ptr(),
+                                             n, records.data_ptr(), ext.data_ptr(), s),
+                   "zp_parse_batch_device")
+        _lib.check(lib.zp_extract_columns_device(arena.data_ptr(), offs.data_ptr(),
+                                                 lens.data_ptr(), records.data_ptr(), n, ptrs, s),
+                   "zp_extract_columns_device")
+    paths = {"fused": fused, "split": split}
+    if mode != "auto":
+        paths[mode]()
+        return records, ext, {k: out[k] for k in names}
+    st = _auto.setdefault(_auto_key(arena, n, names), {"fused": [], "split": [], "choice": None})
+    if st["choice"] is not None or n == 0:
+        paths[st["choice"] or "fused"]()
+        return records, ext, {k: out[k] for k in names}
+    # still timing: the path with fewer samples, bracketed by events
+    which = "fused" if len(st["fused"]) <= len(st["split"]) else "split"
+    ts = torch.cuda.ExternalStream(stream, device=d) if stream is not None else \
+        torch.cuda.current_stream(d)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(ts)
+    paths[which]()
+    b.record(ts)
+    b.synchronize()
+    st[which].append(a.elapsed_time(b))
+    if len(st["fused"]) >= _AUTO_TRIALS and len(st["split"]) >= _AUTO_TRIALS:
+        st["choice"] = min(("fused", "split"), key=lambda k: float(np.median(st[k])))
     return records, ext, {k: out[k] for k in names}

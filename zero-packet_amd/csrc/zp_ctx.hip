@@ -477,6 +477,7 @@ extern "C" void zp__one_stamps(zp_ctx* c, uint64_t* out) {
     memcpy(out, c->one_h + 32, 32);
     memcpy(out + 4, c->one_h + 24, 8);
     memcpy(out + 5, c->one_h + 16, 8);      // ZP_ONE_TWICE: the second pass
+    memcpy(out + 6, c->one_h + 256, 8 * 8);  // phase stamps (OSTAMP 0-7)
 }
 #endif
 

@@ -131,6 +131,19 @@ extern "C" int zp_stamps_set(void* p) {
 #else
 #define STAMP(i) do {} while (0)
 #endif
+// Diagnostic build only (-DZP_ONE_STAMPS): the resident zp_parse_one server's
+// phase stamps, written into its host block at 256 + 8 i (zp__one_stamps).
+#ifdef ZP_ONE_STAMPS
+#define OSTAMP(i)                                                              \
+    do {                                                                       \
+        if (SYS && sysbase && lane == 0)                                       \
+            __hip_atomic_store((uint64_t*)(sysbase + 256 + 8 * (i)),           \
+                               __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, \
+                               __HIP_MEMORY_SCOPE_SYSTEM);                     \
+    } while (0)
+#else
+#define OSTAMP(i) do {} while (0)
+#endif
 
 // --------------------------------------------------------------------------
 // Frame view: LDS window (16-B cells, chunk c of frame f at win[c][f ^ c]:
@@ -975,6 +988,7 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
     }
 #endif
     STAMP(5);
+    OSTAMP(5);
     if (!s.live) return;
     // The frame's stream sum covers the whole chunks [A & ~15, E16):
     // L4 sum = that - V[A & ~15, A + l4) - V[E, E16).
@@ -1005,6 +1019,7 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
         }
     }
     STAMP(6);
+    OSTAMP(6);
     static_assert(sizeof(zp_record) == 8 && sizeof(zp_ext_offsets) == 16, "8-B records");
     const uint64_t p = s.tile * 64 + lane;
 #ifdef ZP_ABL_NOREC
@@ -1106,6 +1121,7 @@ __device__ __forceinline__ void parse_tile(uint64_t t, uint32_t len, uintptr_t g
     TileState s;
     tile_setup(s, t, len, ga, n, lane, lds);
     STAMP(1);
+    OSTAMP(1);
     // stream: one group of ZP_G items per iteration (group 0 outside the
     // loop, so no load is in flight across the loop back-edge)
 #if ZP_SMALL_G
@@ -1116,6 +1132,7 @@ __device__ __forceinline__ void parse_tile(uint64_t t, uint32_t len, uintptr_t g
         uint32_t ks[ZP_SMALL_G];
         issue_group<ZP_SMALL_G, false, SYS>(0, s.nitems, s.cur, s.R, lane, fallback, vs, ks, sysbase);
         STAMP(2);
+        OSTAMP(2);
         consume_group<ZP_SMALL_G>(0, s.nitems, lane, vs, ks, win, tail, lds.cend, s.run);
     } else
 #endif
@@ -1166,8 +1183,10 @@ __device__ __forceinline__ void parse_tile(uint64_t t, uint32_t len, uintptr_t g
     __builtin_amdgcn_s_setprio(0);             // walk at priority 0 ...
 #endif
     STAMP(3);
+    OSTAMP(3);
     tile_finish<COLS, SYS>(s, n, lane, lds, records, ext, cols, sysbase, rec_out);
     STAMP(4);
+    OSTAMP(4);
 }
 
 template <bool COLS>
