@@ -79,7 +79,7 @@ def extract(arena, offs, lens, records, names=None, out=None, stream=None, check
 # column requests run faster as parse + extract (round 4/5: c3 with all 29
 # columns +2-3 % fused; c4/c5/c6 -11 to -23 %). The library
 # times both paths on the first calls of a workload and keeps the faster one.
-_AUTO_TRIALS = 2
+_AUTO_TRIALS = 5           # timed calls per path; the first of each is dropped (warm-up)
 _auto = {}
 
 
@@ -102,7 +102,8 @@ def parse_with_columns(arena, offs, lens, names=None, records=None, ext=None, ou
     "split" = zp_parse_batch_device then zp_extract_columns_device on the same
     stream; "auto" (default) = the faster of the two for this workload (device,
     column set, batch-size octave), timed with HIP events on the launch stream
-    over the first 2 calls of each path (those calls synchronise), then kept."""
+    over the first 5 calls of each path (those calls synchronise; the first of
+    each is not counted), then kept."""
     for t in (arena, offs, lens):
         if not t.is_cuda:
             raise RuntimeError("columns.parse_with_columns needs device tensors (no CPU fallback)")
@@ -156,5 +157,5 @@ def parse_with_columns(arena, offs, lens, names=None, records=None, ext=None, ou
     b.synchronize()
     st[which].append(a.elapsed_time(b))
     if len(st["fused"]) >= _AUTO_TRIALS and len(st["split"]) >= _AUTO_TRIALS:
-        st["choice"] = min(("fused", "split"), key=lambda k: float(np.median(st[k])))
+        st["choice"] = min(("fused", "split"), key=lambda k: float(np.median(st[k][1:])))
     return records, ext, {k: out[k] for k in names}

@@ -396,7 +396,11 @@ static int one_via_server(zp_ctx* c, uint32_t len) {
 #else
                 (void)ack;
 #endif
+                int prev = 0;
+                (void)hipGetDevice(&prev);
+                (void)hipSetDevice(c->device);
                 const int rc = zp__one_server_launch(c->one_d, c->one_seq, ticks, c->srv);
+                (void)hipSetDevice(prev);
                 if (rc) return rc;
             } else if (q != hipErrorNotReady) {
                 snprintf(g_ctx_error, ERRBUF_LEN, "zp_parse_one server: %s", hipGetErrorString(q));
@@ -424,41 +428,50 @@ static int one_via_server(zp_ctx* c, uint32_t len) {
 extern "C" int zp_parse_one(zp_ctx* c, const uint8_t* frame, uint64_t len,
                             zp_record* record, zp_ext_offsets* ext) {
     if (!c || !record || len > 0xFFFFFFFFull || (!frame && len)) return -1;
-    int prev = 0;
-    (void)hipGetDevice(&prev);
-    if (hipSetDevice(c->device) != hipSuccess) return -2;
-    if (len > ONE_MAX || !one_block(c)) {
-        (void)hipSetDevice(prev);
-        uint64_t off = 0;
-        uint32_t l = (uint32_t)len;
-        static const uint8_t empty[16] = {0};
-        if (ext) memset(ext, 0, 2 * sizeof(zp_ext_offsets));   // unflagged entries: zero
-        const int rc = zp_parse_batch_host(c, frame ? frame : empty, len, &off, &l, 1, record, ext);
-        return rc ? rc : (int)zp_rec_err(*record);
-    }
-    uint8_t* h = c->one_h;
-    if (len) memcpy(h + ONE_FRAME, frame, len);
     int rc;
-    if (c->one_idle_us) {
+    uint8_t* h = c->one_h;
+    if (h && len <= ONE_MAX && c->one_idle_us && c->srv_live &&
+        mono_ns() - c->srv_seen_ns < (int64_t)c->one_idle_us * 1000 - ONE_MARGIN_NS) {
+        // The fast path: the server surely runs (it answered less than its
+        // idle timeout ago), so no HIP call at all: copy, doorbell, spin.
+        if (len) memcpy(h + ONE_FRAME, frame, len);
         rc = one_via_server(c, (uint32_t)len);
     } else {
-        const uint64_t at = ONE_FRAME;
-        const uint32_t l = (uint32_t)len;
-        memcpy(h + ONE_OFFS, &at, 8);
-        memcpy(h + ONE_LENS, &l, 4);
-        rc = zp_parse_batch_device(c->one_d, (const uint64_t*)(c->one_d + ONE_OFFS),
-                                   (const uint32_t*)(c->one_d + ONE_LENS), 1,
-                                   (zp_record*)(c->one_d + ONE_REC),
-                                   (zp_ext_offsets*)(c->one_d + ONE_EXT), c->s[0]);
-        if (!rc) {
-            const hipError_t e = hipStreamSynchronize(c->s[0]);
-            if (e != hipSuccess) {
-                snprintf(g_ctx_error, ERRBUF_LEN, "zp_parse_one: %s", hipGetErrorString(e));
-                rc = -2;
+        int prev = 0;
+        (void)hipGetDevice(&prev);
+        if (hipSetDevice(c->device) != hipSuccess) return -2;
+        if (len > ONE_MAX || !one_block(c)) {
+            (void)hipSetDevice(prev);
+            uint64_t off = 0;
+            uint32_t l = (uint32_t)len;
+            static const uint8_t empty[16] = {0};
+            if (ext) memset(ext, 0, 2 * sizeof(zp_ext_offsets));   // unflagged entries: zero
+            const int r2 = zp_parse_batch_host(c, frame ? frame : empty, len, &off, &l, 1, record, ext);
+            return r2 ? r2 : (int)zp_rec_err(*record);
+        }
+        h = c->one_h;
+        if (len) memcpy(h + ONE_FRAME, frame, len);
+        if (c->one_idle_us) {
+            rc = one_via_server(c, (uint32_t)len);
+        } else {
+            const uint64_t at = ONE_FRAME;
+            const uint32_t l = (uint32_t)len;
+            memcpy(h + ONE_OFFS, &at, 8);
+            memcpy(h + ONE_LENS, &l, 4);
+            rc = zp_parse_batch_device(c->one_d, (const uint64_t*)(c->one_d + ONE_OFFS),
+                                       (const uint32_t*)(c->one_d + ONE_LENS), 1,
+                                       (zp_record*)(c->one_d + ONE_REC),
+                                       (zp_ext_offsets*)(c->one_d + ONE_EXT), c->s[0]);
+            if (!rc) {
+                const hipError_t e = hipStreamSynchronize(c->s[0]);
+                if (e != hipSuccess) {
+                    snprintf(g_ctx_error, ERRBUF_LEN, "zp_parse_one: %s", hipGetErrorString(e));
+                    rc = -2;
+                }
             }
         }
+        (void)hipSetDevice(prev);
     }
-    (void)hipSetDevice(prev);
     if (rc) return rc;
     memcpy(record, h + ONE_REC, sizeof(zp_record));
     if (ext) {
@@ -477,7 +490,7 @@ extern "C" void zp__one_stamps(zp_ctx* c, uint64_t* out) {
     memcpy(out, c->one_h + 32, 32);
     memcpy(out + 4, c->one_h + 24, 8);
     memcpy(out + 5, c->one_h + 16, 8);      // ZP_ONE_TWICE: the second pass
-    memcpy(out + 6, c->one_h + 256, 8 * 8);  // phase stamps (OSTAMP 0-7)
+    memcpy(out + 6, c->one_h + ONE_FRAME + ONE_MAX, 8 * 8);  // phase stamps (OSTAMP 0-7)
 }
 #endif
 

@@ -132,12 +132,13 @@ extern "C" int zp_stamps_set(void* p) {
 #define STAMP(i) do {} while (0)
 #endif
 // Diagnostic build only (-DZP_ONE_STAMPS): the resident zp_parse_one server's
-// phase stamps, written into its host block at 256 + 8 i (zp__one_stamps).
+// phase stamps, written into the spare 64 B at the end of its host block
+// (128 + 64 KiB + 8 i, past the largest frame; zp__one_stamps).
 #ifdef ZP_ONE_STAMPS
 #define OSTAMP(i)                                                              \
     do {                                                                       \
         if (SYS && sysbase && lane == 0)                                       \
-            __hip_atomic_store((uint64_t*)(sysbase + 256 + 8 * (i)),           \
+            __hip_atomic_store((uint64_t*)(sysbase + 65664 + 8 * (i)),         \
                                __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, \
                                __HIP_MEMORY_SCOPE_SYSTEM);                     \
     } while (0)
@@ -966,7 +967,8 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
     // The common shape straight-line when most of the wave has it
     // (wave-uniform test); the rest of the frames take the general walk.
     const bool probe = s.live && v4_probe(fv, pr);
-    if (__builtin_popcountll(__ballot(probe)) >= 32) {
+    // (SYS: the one-frame tile of the zp_parse_one server takes it alone)
+    if (__builtin_popcountll(__ballot(probe)) >= (SYS ? 1 : 32)) {
         if (probe) done = fast_v4(fv, pr, w);
     }
 #endif
@@ -1363,11 +1365,13 @@ zp_one_server_kernel(uint8_t* blk, uint32_t seq, uint64_t idle) {
             // or write back
 #ifdef ZP_ONE_ACK16
             zp_u32x2 rq = {0u, 0u};
-            parse_tile<false, false, true>(0, blen, (uintptr_t)(blk + ZP_ONE_FRAME), 1, lane, lds,
+            parse_tile<false, false, true>(0, lane == 0 ? blen : 0u, (uintptr_t)(blk + ZP_ONE_FRAME), 1,
+                                    lane, lds,
                                     (zp_record*)(blk + ZP_ONE_REC),
                                     (zp_ext_offsets*)(blk + ZP_ONE_EXT), none, (uintptr_t)blk, &rq);
 #else
-            parse_tile<false, false, true>(0, blen, (uintptr_t)(blk + ZP_ONE_FRAME), 1, lane, lds,
+            parse_tile<false, false, true>(0, lane == 0 ? blen : 0u, (uintptr_t)(blk + ZP_ONE_FRAME), 1,
+                                    lane, lds,
                                     (zp_record*)(blk + ZP_ONE_REC),
                                     (zp_ext_offsets*)(blk + ZP_ONE_EXT), none, (uintptr_t)blk);
 #endif
@@ -1382,7 +1386,8 @@ zp_one_server_kernel(uint8_t* blk, uint32_t seq, uint64_t idle) {
             {
                 wave_lds_fence();
                 const uint64_t t2 = __builtin_amdgcn_s_memrealtime();
-                parse_tile<false, false, true>(0, blen, (uintptr_t)(blk + ZP_ONE_FRAME), 1, lane, lds,
+                parse_tile<false, false, true>(0, lane == 0 ? blen : 0u, (uintptr_t)(blk + ZP_ONE_FRAME), 1,
+                                    lane, lds,
                                         (zp_record*)(blk + ZP_ONE_REC),
                                         (zp_ext_offsets*)(blk + ZP_ONE_EXT), none, (uintptr_t)blk);
                 // the second pass's ticks (bell_to_tile stays the first pass)
