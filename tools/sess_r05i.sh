@@ -1,0 +1,4 @@
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_parity.py -k "parse_one or golden" > gpurun_out/r05i_tests_po.log 2>&1 || exit $?
+timeout -k 10 300 python tools/parse_one_latency.py --calls 5000 > gpurun_out/r05i_lat.log 2>&1 || exit $?
+timeout -k 10 200 python tools/parse_one_latency.py --calls 3000 --modes 5000 --threads 1 --lib tools/variants/stamps > gpurun_out/r05i_lat_stamps.log 2>&1 || exit $?

@@ -366,23 +366,7 @@ static int one_via_server(zp_ctx* c, uint32_t len) {
     const int64_t t0 = now;
     int64_t next_check = t0 + 200000;                        // 200 us
     for (uint32_t spin = 1;; ++spin) {
-#ifdef ZP_ONE_ACK16
-        // {record, seq, check} written by one 16-B store (zp_parse.hip)
-        {
-            volatile uint32_t* a16 = (volatile uint32_t*)(c->one_h + ONE_ACK);   // ZP_ONE_ACK16_OFF
-            if (a16[2] == seq) {
-                __atomic_thread_fence(__ATOMIC_ACQUIRE);
-                const uint32_t f = a16[0], o = a16[1], q = a16[2], k = a16[3];
-                if (q == seq && k == (f ^ o ^ q ^ 0xA5A5A5A5u)) {
-                    memcpy(c->one_h + ONE_REC, &f, 4);
-                    memcpy(c->one_h + ONE_REC + 4, &o, 4);
-                    break;
-                }
-            }
-        }
-#else
         if (__atomic_load_n(ack, __ATOMIC_ACQUIRE) == seq) break;
-#endif
         __builtin_ia32_pause();
         if ((spin & 1023u) == 0) {
             now = mono_ns();
@@ -391,11 +375,7 @@ static int one_via_server(zp_ctx* c, uint32_t len) {
             // timeout): then its stream is done and the request still open.
             const hipError_t q = hipStreamQuery(c->srv);
             if (q == hipSuccess) {
-#ifndef ZP_ONE_ACK16
                 if (__atomic_load_n(ack, __ATOMIC_ACQUIRE) == seq) break;
-#else
-                (void)ack;
-#endif
                 int prev = 0;
                 (void)hipGetDevice(&prev);
                 (void)hipSetDevice(c->device);
@@ -489,7 +469,6 @@ extern "C" int zp_parse_one(zp_ctx* c, const uint8_t* frame, uint64_t len,
 extern "C" void zp__one_stamps(zp_ctx* c, uint64_t* out) {
     memcpy(out, c->one_h + 32, 32);
     memcpy(out + 4, c->one_h + 24, 8);
-    memcpy(out + 5, c->one_h + 16, 8);      // ZP_ONE_TWICE: the second pass
     memcpy(out + 6, c->one_h + ONE_FRAME + ONE_MAX, 8 * 8);  // phase stamps (OSTAMP 0-7)
 }
 #endif

@@ -164,6 +164,7 @@ struct FrameView {
     const uint4* win;        // this wave's window, [ZP_WIN_CH][64]
 #if ZP_REGION
     const uint32_t* reg;     // ZP_REGION: this lane's window, ZP_WIN / 4 dwords from A & ~15
+    bool region;             // reg is set (a constant per kernel: the one-frame server reads the cells)
 #endif
     const uint8_t* g;        // frame in global memory
     uint32_t lane;
@@ -180,14 +181,17 @@ struct FrameView {
 
 __device__ __forceinline__ uint4 win_chunk(const FrameView& f, uint32_t c) {
 #if ZP_REGION
-    return make_uint4(f.reg[4 * c], f.reg[4 * c + 1], f.reg[4 * c + 2], f.reg[4 * c + 3]);
+    if (f.region) return make_uint4(f.reg[4 * c], f.reg[4 * c + 1], f.reg[4 * c + 2], f.reg[4 * c + 3]);
+    return f.win[c * 64 + (f.lane ^ c)];
 #else
     return f.win[c * 64 + (f.lane ^ c)];
 #endif
 }
 __device__ __forceinline__ uint32_t win_dw(const FrameView& f, uint32_t d) {
 #if ZP_REGION
-    return f.reg[d];
+    if (f.region) return f.reg[d];
+    const uint32_t c = d >> 2;
+    return ((const uint32_t*)&f.win[c * 64 + (f.lane ^ c)])[d & 3];
 #else
     const uint32_t c = d >> 2;
     return ((const uint32_t*)&f.win[c * 64 + (f.lane ^ c)])[d & 3];
@@ -911,8 +915,7 @@ template <bool COLS, bool SYS = false>
 __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, WaveLds& lds,
                                             zp_record* __restrict__ records,
                                             zp_ext_offsets* __restrict__ ext,
-                                            const ColPtrs& cols, uintptr_t sysbase = 0,
-                                            zp_u32x2* rec_out = nullptr) {
+                                            const ColPtrs& cols, uintptr_t sysbase = 0) {
     uint4* tail = &lds.win[ZP_WIN_CH * 64];
     const uint8_t* g = (const uint8_t*)s.ga;
 #ifdef ZP_STAMPS
@@ -930,9 +933,15 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
     fv.sysbase = SYS ? sysbase : 0;
 #if ZP_REGION
     // the frame's cells and last chunk to registers, then its window to the
-    // lane's private region (it overlays the cells and part of the tails)
+    // lane's private region (it overlays the cells and part of the tails);
+    // the one-frame tile of the zp_parse_one server (SYS) reads the cells
+    // where the stream put them (the copy is latency on its critical path)
     uint4 mytail;
-    {
+    fv.region = !SYS;
+    if (SYS) {
+        mytail = tail[s.rank & 63u];
+        fv.reg = nullptr;
+    } else {
         static_assert(64 * ZP_RSTRIDE * 4 <= (ZP_WIN_CH + 1) * 64 * 16, "regions fit the window LDS");
         const uint32_t rk = s.rank & 63u;
         uint4 cell[ZP_WIN_CH];
@@ -1041,8 +1050,7 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
 #else
         if (SYS) {
             const zp_u32x2 q = zp_pack(rec);
-            if (rec_out) *rec_out = q;                   // the caller stores it (with its ack)
-            else st_sys8(records + p, ((uint64_t)q.y << 32) | q.x);
+            st_sys8(records + p, ((uint64_t)q.y << 32) | q.x);
         } else {
             __builtin_nontemporal_store(zp_pack(rec), (zp_u32x2*)(records + p));
         }
@@ -1106,8 +1114,7 @@ __device__ __forceinline__ void parse_tile(uint64_t t, uint32_t len, uintptr_t g
                                            int lane, WaveLds& lds,
                                            zp_record* __restrict__ records,
                                            zp_ext_offsets* __restrict__ ext,
-                                           const ColPtrs& cols, uintptr_t sysbase = 0,
-                                           zp_u32x2* rec_out = nullptr) {
+                                           const ColPtrs& cols, uintptr_t sysbase = 0) {
 #ifdef ZP_STAMPS
     const uint64_t wave_id = t;
 #endif
@@ -1186,7 +1193,7 @@ __device__ __forceinline__ void parse_tile(uint64_t t, uint32_t len, uintptr_t g
 #endif
     STAMP(3);
     OSTAMP(3);
-    tile_finish<COLS, SYS>(s, n, lane, lds, records, ext, cols, sysbase, rec_out);
+    tile_finish<COLS, SYS>(s, n, lane, lds, records, ext, cols, sysbase);
     STAMP(4);
     OSTAMP(4);
 }
@@ -1327,7 +1334,6 @@ extern "C" int zp_parse_batch_columns_device(const uint8_t* arena, const uint64_
 #define ZP_ONE_REC 64        // zp_record (server writes)
 #define ZP_ONE_ACK 80        // uint32_t: seq of the last finished request (server writes)
 #define ZP_ONE_EXT 96        // zp_ext_offsets[2] (server writes)
-#define ZP_ONE_ACK16_OFF 80  // ZP_ONE_ACK16 (A/B): {record, seq, check} in one 16-B store (over ZP_ONE_ACK)
 #define ZP_ONE_FRAME 128     // the frame (host writes)
 #define ZP_ONE_STOP 0xFFFFFFFFu   // doorbell length: leave now
 
@@ -1336,90 +1342,51 @@ zp_one_server_kernel(uint8_t* blk, uint32_t seq, uint64_t idle) {
     __shared__ WaveLds lds;
     const int lane = threadIdx.x & 63;
     const ColPtrs none{};
-    uint64_t last = __builtin_amdgcn_s_memrealtime();
 #ifdef ZP_ONE_STAMPS   // diagnostic build only (tools/parse_one_latency.py --lib)
     uint64_t polls = 0;
 #endif
+    // One system-scope poll of the doorbell in flight, from lane 0 only
+    // (loads of one address from several lanes are not merged and cost
+    // ~0.1 us each). Measured and not kept (profiles/r05_parse_one_server_
+    // iterations.log): four polling waves (7.2 us per call: they slow the
+    // working wave's host accesses), and several polls in flight from this
+    // wave (the compiler waits for all of them at the rotation's head).
+    uint64_t last = __builtin_amdgcn_s_memrealtime();
     for (;;) {
-#ifdef ZP_ONE_STAMPS
-        ++polls;
-#endif
         uint64_t bell = 0;
         if (lane == 0)
             bell = __hip_atomic_load((const uint64_t*)(blk + ZP_ONE_BELL), __ATOMIC_RELAXED,
                                      __HIP_MEMORY_SCOPE_SYSTEM);
         const uint32_t bseq = (uint32_t)__builtin_amdgcn_readlane((uint32_t)(bell >> 32), 0);
         const uint32_t blen = (uint32_t)__builtin_amdgcn_readlane((uint32_t)bell, 0);
-        if (bseq != seq) {                                   // wave-uniform
-            if (blen == ZP_ONE_STOP) break;
+        if (bseq == seq) {
+            if (__builtin_amdgcn_s_memrealtime() - last > idle) break;
+            continue;
+        }
+        if (blen == ZP_ONE_STOP) break;
+        seq = bseq;
+#ifdef ZP_ONE_STAMPS
+        ++polls;
+#endif
+        {                                                    // a request (wave-uniform)
 #ifdef ZP_ONE_STAMPS
             const uint64_t t_bell = __builtin_amdgcn_s_memrealtime();
             const uint64_t c_bell = __builtin_amdgcn_s_memtime();
-#endif
-#ifdef ZP_ONE_ACQ   // A/B only: a cache-wide acquire (the loads are system-scope anyway)
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
 #endif
             __builtin_amdgcn_s_setprio(1);
             // every load of the frame and every store of the results is
             // system-scope (SYS): nothing is left in a cache to invalidate
             // or write back
-#ifdef ZP_ONE_ACK16
-            zp_u32x2 rq = {0u, 0u};
-            parse_tile<false, false, true>(0, lane == 0 ? blen : 0u, (uintptr_t)(blk + ZP_ONE_FRAME), 1,
-                                    lane, lds,
-                                    (zp_record*)(blk + ZP_ONE_REC),
-                                    (zp_ext_offsets*)(blk + ZP_ONE_EXT), none, (uintptr_t)blk, &rq);
-#else
             parse_tile<false, false, true>(0, lane == 0 ? blen : 0u, (uintptr_t)(blk + ZP_ONE_FRAME), 1,
                                     lane, lds,
                                     (zp_record*)(blk + ZP_ONE_REC),
                                     (zp_ext_offsets*)(blk + ZP_ONE_EXT), none, (uintptr_t)blk);
-#endif
-#ifdef ZP_ONE_REL   // A/B only: a cache-wide release
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-#endif
 #ifdef ZP_ONE_STAMPS
             const uint64_t t_tile = __builtin_amdgcn_s_memrealtime();
             const uint64_t c_tile = __builtin_amdgcn_s_memtime();
 #endif
-#ifdef ZP_ONE_TWICE   // diagnostic: the same tile again, warm (instruction cache, LDS)
-            {
-                wave_lds_fence();
-                const uint64_t t2 = __builtin_amdgcn_s_memrealtime();
-                parse_tile<false, false, true>(0, lane == 0 ? blen : 0u, (uintptr_t)(blk + ZP_ONE_FRAME), 1,
-                                    lane, lds,
-                                        (zp_record*)(blk + ZP_ONE_REC),
-                                        (zp_ext_offsets*)(blk + ZP_ONE_EXT), none, (uintptr_t)blk);
-                // the second pass's ticks (bell_to_tile stays the first pass)
-                if (lane == 0) st_sys8(blk + 16, __builtin_amdgcn_s_memrealtime() - t2);
-            }
-#endif
-#ifdef ZP_ONE_ACK16
-            // The record and the ack leave in ONE 16-B system-scope store
-            // from lane 0 ({record, seq, check}; the host accepts it when the
-            // check matches), so only chain entries, when the record flags
-            // any, are waited for before it.
-            {
-                const uint32_t fl = __builtin_amdgcn_readlane(rq.x, 0);
-                const uint32_t of = __builtin_amdgcn_readlane(rq.y, 0);
-                // zp_rec_chain_inline (include/zero_packet.h): no entry written
-                const bool inl = ((fl >> 24) & 3u) != ZP_ETH_CODE_FAR &&
-                                 (fl & (ZP_F_EXT | ZP_F_IP_IN_IP)) == ZP_F_EXT &&
-                                 (of & ZP_CHAIN_INLINE) != 0;
-                const bool chains = (fl >> 26) == 0 &&
-                    ((fl & ZP_F_INNER_EXT) || ((fl & ZP_F_EXT) && !inl));
-                if (chains) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                if (lane == 0) {
-                    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-                        (void*)blk, (short)0, (int)ZP_SYS_BYTES, 0x00020000);
-                    const zp_u32x4 q = {fl, of, bseq, fl ^ of ^ bseq ^ 0xA5A5A5A5u};
-                    __builtin_amdgcn_raw_buffer_store_b128(q, r, ZP_ONE_ACK16_OFF, 0, 1 | 16);
-                }
-            }
-#else
             // record + chains (system-scope stores) complete before the ack
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
 #ifdef ZP_ONE_STAMPS
             if (lane == 0) {
                 st_sys8(blk + 32, t_bell);
@@ -1431,18 +1398,12 @@ zp_one_server_kernel(uint8_t* blk, uint32_t seq, uint64_t idle) {
             polls = 0;
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
-#ifndef ZP_ONE_ACK16
             if (lane == 0)
                 __hip_atomic_store((uint32_t*)(blk + ZP_ONE_ACK), bseq, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_SYSTEM);
-#endif
-            seq = bseq;
             wave_lds_fence();                                 // LDS reused by the next request
             last = __builtin_amdgcn_s_memrealtime();
-            continue;
         }
-        if (__builtin_amdgcn_s_memrealtime() - last > idle) break;
-        __builtin_amdgcn_s_sleep(2);
     }
 }
 
