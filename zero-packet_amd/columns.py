@@ -77,9 +77,9 @@ def extract(arena, offs, lens, records, names=None, out=None, stream=None, check
 # Path choice of parse_with_columns(mode="auto") per workload key: the fused
 # kernel (one pass) wins on most traffic, but plain IPv4 frames with wide
 # column requests run faster as parse + extract (round 4/5: c3 with all 29
-# columns +2-3 % fused; c4/c5/c6 -11 to -23 %). The library
-# times both paths on the first calls of a workload and keeps the faster one.
-_AUTO_TRIALS = 5           # timed calls per path; the first of each is dropped (warm-up)
+# columns +2-5 % fused; c4/c5/c6 -11 to -23 %). The library
+# times both paths on the first call of a workload and keeps the faster one.
+_AUTO_REPS = 2             # timed back-to-back runs per path (after one warm-up run)
 _auto = {}
 
 
@@ -89,9 +89,8 @@ def _auto_key(arena, n, names):
 
 def auto_choice(arena, n, names):
     """The path parse_with_columns(mode="auto") uses for this workload key
-    (None while it is still timing both)."""
-    st = _auto.get(_auto_key(arena, n, names))
-    return st["choice"] if st else None
+    (None before its first call)."""
+    return _auto.get(_auto_key(arena, n, names))
 
 
 def parse_with_columns(arena, offs, lens, names=None, records=None, ext=None, out=None,
@@ -101,9 +100,9 @@ def parse_with_columns(arena, offs, lens, names=None, records=None, ext=None, ou
     mode: "fused" = zp_parse_batch_columns_device (one pass over the frames);
     "split" = zp_parse_batch_device then zp_extract_columns_device on the same
     stream; "auto" (default) = the faster of the two for this workload (device,
-    column set, batch-size octave), timed with HIP events on the launch stream
-    over the first 5 calls of each path (those calls synchronise; the first of
-    each is not counted), then kept."""
+    column set, batch-size octave): its first call runs each path once, then
+    twice back to back between HIP events on the launch stream, keeps the
+    faster, and synchronises; later calls of the workload run that path."""
     for t in (arena, offs, lens):
         if not t.is_cuda:
             raise RuntimeError("columns.parse_with_columns needs device tensors (no CPU fallback)")
@@ -142,20 +141,25 @@ def parse_with_columns(arena, offs, lens, names=None, records=None, ext=None, ou
     if mode != "auto":
         paths[mode]()
         return records, ext, {k: out[k] for k in names}
-    st = _auto.setdefault(_auto_key(arena, n, names), {"fused": [], "split": [], "choice": None})
-    if st["choice"] is not None or n == 0:
-        paths[st["choice"] or "fused"]()
+    key = _auto_key(arena, n, names)
+    choice = _auto.get(key)
+    if choice is None and n:
+        # First call of this workload: each path once to warm up, then twice
+        # back to back between two events (as a stream of calls runs), and
+        # the faster is kept. Every run writes the same outputs.
+        ts = torch.cuda.ExternalStream(stream, device=d) if stream is not None else \
+            torch.cuda.current_stream(d)
+        ms = {}
+        for k in ("fused", "split"):
+            paths[k]()
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(ts)
+            for _ in range(_AUTO_REPS):
+                paths[k]()
+            b.record(ts)
+            b.synchronize()
+            ms[k] = a.elapsed_time(b)
+        choice = _auto[key] = min(ms, key=ms.get)
         return records, ext, {k: out[k] for k in names}
-    # still timing: the path with fewer samples, bracketed by events
-    which = "fused" if len(st["fused"]) <= len(st["split"]) else "split"
-    ts = torch.cuda.ExternalStream(stream, device=d) if stream is not None else \
-        torch.cuda.current_stream(d)
-    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    a.record(ts)
-    paths[which]()
-    b.record(ts)
-    b.synchronize()
-    st[which].append(a.elapsed_time(b))
-    if len(st["fused"]) >= _AUTO_TRIALS and len(st["split"]) >= _AUTO_TRIALS:
-        st["choice"] = min(("fused", "split"), key=lambda k: float(np.median(st[k][1:])))
+    paths[choice or "fused"]()
     return records, ext, {k: out[k] for k in names}
