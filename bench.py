@@ -278,7 +278,11 @@ def config5_leg(zp, total, steps, warmup, world, rank, dev, barrier, coll_dev):
     rows = gather_rows([first, end, nbytes, errs, kmean, elapsed], world, rank, coll_dev)
     t = float(rows[:, 5].max())
     job_bytes = int(rows[:, 2].sum())
+    # HBM bytes per launch from the committed PMC pass of the whole stream on
+    # one GPU (tools/pmc_traffic.sh <round> c5), when this run is that workload
+    traffic, traffic_src = pmc_traffic("c5", n, nbytes) if world == 1 else (None, None)
     return {
+        "traffic": traffic, "traffic_source": traffic_src,
         "workload": WORKLOADS["c5"].replace(" shard", "") + f", {total} frames split {world} ways",
         "frames_total": total, "bytes_total": job_bytes, "scaling": "strong",
         "steps": steps, "warmup": warmup, "ms_per_step": round(t / steps * 1e3, 4),

@@ -84,7 +84,16 @@ _auto = {}
 
 
 def _auto_key(arena, n, names):
-    return (arena.device.index, tuple(sorted(names)), max(n, 1).bit_length())
+    # the arena buffer too: traffic of another shape arrives in another buffer
+    # (c3 and c4 batches of one size want different paths, tools/cols_policy.py)
+    return (arena.device.index, arena.data_ptr(), tuple(sorted(names)), max(n, 1).bit_length())
+
+
+def reset_auto():
+    """Forgets every choice of parse_with_columns(mode="auto") (the traffic in
+    a reused arena changed shape): the next call of each workload times both
+    paths again."""
+    _auto.clear()
 
 
 def auto_choice(arena, n, names):
@@ -100,7 +109,8 @@ def parse_with_columns(arena, offs, lens, names=None, records=None, ext=None, ou
     mode: "fused" = zp_parse_batch_columns_device (one pass over the frames);
     "split" = zp_parse_batch_device then zp_extract_columns_device on the same
     stream; "auto" (default) = the faster of the two for this workload (device,
-    column set, batch-size octave): its first call runs each path once, then
+    arena buffer, column set, batch-size octave; reset_auto() forgets the
+    choices): its first call runs each path once, then
     twice back to back between HIP events on the launch stream, keeps the
     faster, and synchronises; later calls of the workload run that path."""
     for t in (arena, offs, lens):
