@@ -546,7 +546,7 @@ __device__ __forceinline__ void walk_frame(FrameView& f, Walk& w) {
                     const uint32_t hv = (ihl == 20 && pos + 20 <= f.wlen)
                                             ? wsum4<5>(f, pos + f.shift) : sumV(f, pos, pos + ihl);
 #endif
-                    if (!(hv != 0 && hv % 65535u == 0)) { err = ZP_ERR_IPV4_CHECKSUM; goto done; }
+                    if (!nz_mod65535_zero(hv)) { err = ZP_ERR_IPV4_CHECKSUM; goto done; }
                     proto = rd8(f, pos + 9);
                     pp = pos + ihl;
                     if (level == 0) r.flags |= ZP_F_IPV4;
@@ -707,7 +707,7 @@ __device__ __forceinline__ bool fast_v4(const FrameView& f, const Probe& pr, Wal
     const bool tcp = proto == 6, udp = proto == 17, ic4 = proto == 1;
     const uint32_t t = wbe16(f, tcp ? 46u : udp ? 38u : 34u);       // one L4 word
     bool ok = v4_probe(f, pr) && pr.t1 == len - 14 &&              // parser.rs:188-212
-              hv != 0 && hv % 65535u == 0 && (tcp || udp || ic4);
+              nz_mod65535_zero(hv) && (tcp || udp || ic4);
     ok = ok && (tcp ? (t >> 12) >= 5 && (t & 0xFFu) != 0             // parser.rs:237-247
               : udp ? t == len - 34                                  // parser.rs:258-263
                     : icmpv4_type_ok(t >> 8) && (t & 0xFFu) <= 15);  // parser.rs:273-283
@@ -757,7 +757,7 @@ __device__ __forceinline__ IpLevel ip_level(const FrameView& f, uint32_t pos, bo
     const uint32_t tl = wbe16(f, pos + 2);
     const uint32_t p4 = wb8(f, pos + 9), p6 = wb8(f, pos + 6);
     const uint32_t hv = wsum4<5>(f, pos + f.shift);                      // ipv4.rs:262-264
-    const bool ok4 = pos + 20 <= f.len && b0 == 0x45 && tl == sl && hv != 0 && hv % 65535u == 0;
+    const bool ok4 = pos + 20 <= f.len && b0 == 0x45 && tl == sl && nz_mod65535_zero(hv);
     const bool ext6 = p6 == 0 || p6 == 43 || p6 == 44 || p6 == 51 || p6 == 60;  // headers.rs:73-86
     const bool ok6 = pos + 40 <= f.len && (b0 >> 4) == 6 && !ext6;
     IpLevel L;
@@ -875,7 +875,7 @@ __device__ __forceinline__ bool tiny_tile(uint64_t tile, uint32_t len, uintptr_t
                             sad16(f[8] & 0xFFFFu, 0u))))));            // bytes 14..33
     const uint32_t t = tiny_be16(f, tcp ? 46u : udp ? 38u : 34u);
     bool ok = tiny_be16(f, 12) == 0x0800 && ((f[3] >> 16) & 0xFFu) == 0x45 &&
-              tiny_be16(f, 16) == 50u && hv != 0 && hv % 65535u == 0 && (tcp || udp || ic4);
+              tiny_be16(f, 16) == 50u && nz_mod65535_zero(hv) && (tcp || udp || ic4);
     ok = ok && (tcp ? (t >> 12) >= 5 && (t & 0xFFu) != 0
               : udp ? t == 30u
                     : icmpv4_type_ok(t >> 8) && (t & 0xFFu) <= 15);
