@@ -80,6 +80,7 @@
 //   ZP_ABL_NOSCAN     no per-item wave scan (zp_stream.h)
 //   ZP_ABL_EXTRA=n    n extra dependent VALU per stream item (zp_stream.h)
 //   ZP_ABL_NO_IPSUM / ZP_ABL_NO_PSEUDO / ZP_ABL_NO_L4HDR  skip one header sum
+//   ZP_ABL_NO_L1      fast_ip without its second IP level
 //   ZP_ABL_NOREC      no record stores
 //   ZP_ABL_REC4       4-B record stores at 4 * i (wrong contents, timing only)
 //   ZP_STAMPS         per-wave phase timestamps (tools/stamps.py)
@@ -786,7 +787,12 @@ __device__ __forceinline__ bool fast_ip(FrameView& f, const Probe& pr, Walk& w) 
     const IpLevel L0 = ip_level(f, hl, v4o);                            // parse_ipv4 / parse_ipv6
     const bool enc = L0.proto == 4 || L0.proto == 41;                   // parser.rs:134-135
     const bool v4i = L0.proto == 4;
+#ifdef ZP_ABL_NO_L1   // timing ablation only: no second IP level (wrong records)
+    IpLevel L1 = L0;
+    L1.next = L0.next + 20u;
+#else
     const IpLevel L1 = ip_level(f, L0.next, v4i);
+#endif
     ok = ok && L0.ok && (!enc || (L1.ok && L1.proto != 4 && L1.proto != 41));
     const uint32_t proto = enc ? L1.proto : L0.proto;
     const uint32_t pp = enc ? L1.next : L0.next;
@@ -819,7 +825,11 @@ __device__ __forceinline__ bool fast_ip(FrameView& f, const Probe& pr, Walk& w) 
     w.l4 = pp;
     w.v6 = v4 ? 0 : 1;
     w.acc = 0;
+#ifdef ZP_ABL_NO_PSEUDO   // timing ablation only
+    if (false) {
+#else
     if (ok && l4 && !(v4 && ic4)) {
+#endif
         // pseudo-header of the innermost IP (parser.rs:316-333, 341-361)
         const uint32_t plo = v4 ? ipl + 12 : ipl + 8, phi = v4 ? ipl + 20 : ipl + 40;
         uint32_t ps;
@@ -1337,6 +1347,57 @@ extern "C" int zp_parse_batch_columns_device(const uint8_t* arena, const uint64_
 #define ZP_ONE_FRAME 128     // the frame (host writes)
 #define ZP_ONE_STOP 0xFFFFFFFFu   // doorbell length: leave now
 
+// The one frame of a zp_parse_one request, streamed by the server wave: its
+// chunks [A & ~15, E) are contiguous, so lane l of item i simply loads chunk
+// 64 i + l (system-scope; lanes past the frame load nothing), the first
+// ZP_WIN_CH chunks go to the window cells of rank 0, the last to its tail
+// cell, and the frame's word sum is one wave reduction per item. The batch
+// stream's frame-start masks, rank permutes and running scans (tile_setup,
+// issue_group, consume_group) have nothing to do here; the walk, verdict and
+// record store are tile_finish's. Frames <= 64 KiB (ONE_MAX).
+__device__ __forceinline__ void one_frame_tile(uint32_t len, uintptr_t ga, int lane, WaveLds& lds,
+                                               zp_record* records, zp_ext_offsets* ext,
+                                               uintptr_t sysbase) {
+    const ColPtrs none{};
+    const uint32_t shift = (uint32_t)(ga & 15);
+    const uint32_t nch = len >= 64 ? (len + shift + 15) >> 4 : 0u;   // as tile_setup
+    const uintptr_t base = ga & ~(uintptr_t)15;
+    uint32_t total = 0;
+    for (uint32_t i0 = 0; i0 < nch; i0 += 64u * 4u) {
+        uint4 v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t c = i0 + 64u * q + (uint32_t)lane;
+            v[q] = ld_sys16(sysbase, c < nch ? base + 16ull * c : sysbase + 0xFFFFFFF0u);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t c = i0 + 64u * q + (uint32_t)lane;
+            if (c < ZP_WIN_CH && c < nch) lds.win[c * 64 + c] = v[q];   // rank 0's cell c
+            if (c + 1 == nch) lds.win[ZP_WIN_CH * 64] = v[q];            // rank 0's tail
+            uint32_t part = sad16(v[q].x, 0u);
+            part = sad16(v[q].y, part);
+            part = sad16(v[q].z, part);
+            part = sad16(v[q].w, part);
+            total += rdl(wave_scan(c < nch ? part : 0u), 63);
+        }
+    }
+    if (lane == 0) lds.cend[0] = total;
+    wave_lds_fence();
+    TileState s;
+    s.tile = 0;
+    s.ga = ga;
+    s.live = lane == 0;
+    s.len = lane == 0 ? len : 0u;
+    s.shift = shift;
+    s.wlen = s.len < ZP_WIN - shift ? s.len : ZP_WIN - shift;
+    s.giant = false;
+    s.rank = (uint32_t)lane;
+    s.nitems = 0;
+    s.run = 0;
+    tile_finish<false, true>(s, 1, lane, lds, records, ext, none, sysbase);
+}
+
 __global__ void __launch_bounds__(64)
 zp_one_server_kernel(uint8_t* blk, uint32_t seq, uint64_t idle) {
     __shared__ WaveLds lds;
@@ -1377,10 +1438,16 @@ zp_one_server_kernel(uint8_t* blk, uint32_t seq, uint64_t idle) {
             // every load of the frame and every store of the results is
             // system-scope (SYS): nothing is left in a cache to invalidate
             // or write back
+#ifdef ZP_ONE_BATCH_TILE   // A/B: the batch kernel's tile path for the one frame
             parse_tile<false, false, true>(0, lane == 0 ? blen : 0u, (uintptr_t)(blk + ZP_ONE_FRAME), 1,
                                     lane, lds,
                                     (zp_record*)(blk + ZP_ONE_REC),
                                     (zp_ext_offsets*)(blk + ZP_ONE_EXT), none, (uintptr_t)blk);
+#else
+            one_frame_tile(blen, (uintptr_t)(blk + ZP_ONE_FRAME), lane, lds,
+                           (zp_record*)(blk + ZP_ONE_REC), (zp_ext_offsets*)(blk + ZP_ONE_EXT),
+                           (uintptr_t)blk);
+#endif
 #ifdef ZP_ONE_STAMPS
             const uint64_t t_tile = __builtin_amdgcn_s_memrealtime();
             const uint64_t c_tile = __builtin_amdgcn_s_memtime();
