@@ -4,3 +4,4 @@ timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method threa
 timeout -k 10 300 python tools/parse_one_latency.py --calls 5000 > gpurun_out/r05n_lat.log 2>&1 || exit $?
 timeout -k 10 200 python tools/parse_one_latency.py --calls 3000 --modes 5000 --threads 1 --lib tools/variants/stamps > gpurun_out/r05n_lat_stamps.log 2>&1 || exit $?
 timeout -k 10 200 python tools/parse_one_latency.py --calls 5000 --modes 5000 --lib tools/variants/batchtile > gpurun_out/r05n_lat_batchtile.log 2>&1 || exit $?
+timeout -k 10 400 python tools/kbench.py --configs c5,c3,c4,c6 --variants earlyrec,norec --rounds 6 > gpurun_out/r05n_kb_earlyrec.log 2>&1 || exit $?

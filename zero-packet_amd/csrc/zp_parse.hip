@@ -70,6 +70,9 @@
 #ifndef ZP_TAIL_G
 #define ZP_TAIL_G 4          // a tile's last <= this many items as one small group (0: off)
 #endif
+#ifndef ZP_EARLY_REC
+#define ZP_EARLY_REC 1       // the record stored before the verdict (0: after it)
+#endif
 #ifndef ZP_TAIL_G2
 #define ZP_TAIL_G2 1         // ... and the last <= 2 as a pair (c5 -0.5 %, c6 -0.6 %)
 #endif
@@ -1014,6 +1017,15 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
     // The frame's stream sum covers the whole chunks [A & ~15, E16):
     // L4 sum = that - V[A & ~15, A + l4) - V[E, E16).
     zp_rec_full rec = w.rec;
+    const uint64_t p = s.tile * 64 + lane;
+#if ZP_EARLY_REC && !defined(ZP_ABL_NOREC)
+    // The record as the walk left it goes out before the verdict, so its
+    // store's latency overlaps the checksum work instead of ending the wave
+    // (c5 -1.6 %, c3/c4/c6 -0.3 to -0.5 %, profiles/r05_kbench_early_rec.log);
+    // a frame whose L4 checksum then fails stores its error record over it
+    // (same lane, same address: the later store lands last).
+    if (!SYS) __builtin_nontemporal_store(zp_pack(rec), (zp_u32x2*)(records + p));
+#endif
     if (w.pending) {
         bool ok;
         if (s.giant) {
@@ -1037,12 +1049,17 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
         if (!ok) {
             rec = zp_rec_full{};
             rec.err = (uint8_t)(w.v6 ? ZP_ERR_IPV6_L4_CHECKSUM : ZP_ERR_IPV4_L4_CHECKSUM);
+#if ZP_EARLY_REC && !defined(ZP_ABL_NOREC)
+            if (!SYS) __builtin_nontemporal_store(zp_pack(rec), (zp_u32x2*)(records + p));
+#endif
         }
     }
     STAMP(6);
     OSTAMP(6);
     static_assert(sizeof(zp_record) == 8 && sizeof(zp_ext_offsets) == 16, "8-B records");
-    const uint64_t p = s.tile * 64 + lane;
+#if ZP_EARLY_REC
+    if (SYS)
+#endif
 #ifdef ZP_ABL_NOREC
     if (rec.flags == 0xDEADBEEFu)                       // timing ablation: no stores
 #endif
