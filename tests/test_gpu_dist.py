@@ -108,5 +108,7 @@ def test_bench_rccl_path_one_rank():
     assert len(lines) == 1, out.stdout
     r = json.loads(lines[0])
     assert r["n_gpus"] == 1 and r["config"]["dist_backend"] == "nccl"
+    pl = r["roofline"]["placement"]                       # the arena's read probe
+    assert pl["read_gbs"] > 0 and pl["arena_bytes"] >= r["config"]["bytes_per_gpu"] - 16
     assert r["config5"]["rejected_per_rank"] == [0] and r["h2d_d2h_inclusive"]["ranks"] == 1
     assert abs(r["value"] - n * 3 / (r["ms_per_step"] * 3 * 1e-3) / 1e6) < 0.02 * r["value"]

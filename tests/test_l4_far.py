@@ -135,6 +135,9 @@ def test_far_records_decode_exactly(zp):
         assert rc == 0 and all(int(d[k]) == int(rec[k]) for k in FIELDS)
         pd = R.decode(frame, packed, ext)
         assert all(pd[k] == int(rec[k]) for k in FIELDS), (pd, rec)
+        # without entries records.decode walks the chains again, as zp_rec_decode
+        pd = R.decode(frame, packed, None)
+        assert all(pd[k] == int(rec[k]) for k in FIELDS), ("no ext", pd, rec)
         p = zp.PacketParser.from_record(frame, packed, ext)
         offs = _reader_offsets(frame, p)
         assert offs["ethernet"] == 0 and offs["ip_in_ip"] == rec["inner_off"]

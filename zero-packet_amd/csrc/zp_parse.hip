@@ -1021,10 +1021,15 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
 #if ZP_EARLY_REC && !defined(ZP_ABL_NOREC)
     // The record as the walk left it goes out before the verdict, so its
     // store's latency overlaps the checksum work instead of ending the wave
-    // (c5 -1.6 %, c3/c4/c6 -0.3 to -0.5 %, profiles/r05_kbench_early_rec.log);
+    // (two boxes: c5 -1.6 / -0.6 %, c3 -0.3 / +0.6 %, c4 -0.4 / +0.3 %;
+    // profiles/r05_kbench_early_rec.log, r05_kbench_early_rec_k2_norec.log);
     // a frame whose L4 checksum then fails stores its error record over it
     // (same lane, same address: the later store lands last).
+#ifdef ZP_REC_PLAIN   // A/B: default-policy record stores
+    if (!SYS) *(zp_u32x2*)(records + p) = zp_pack(rec);
+#else
     if (!SYS) __builtin_nontemporal_store(zp_pack(rec), (zp_u32x2*)(records + p));
+#endif
 #endif
     if (w.pending) {
         bool ok;
