@@ -3,7 +3,8 @@ hdr_tiles): one wave per tile of 64 frames, the tile read once by 1 KiB
 nontemporal wave loads in groups of 8, then each lane writes back the whole
 64-B sectors covering its frame's first `hdr` bytes (the builder's header
 write-back). Store policies: plain / nt / write-through (agent-scope atomic
-stores) / none. Next to it: the parse kernel and the builder on 4M c3
+stores) / none / plain by the whole wave (coalesced) / plain without the
+read. Next to it: the parse kernel and the builder on 4M c3
 frames of the same box (tools/build_bench.py times the builder).
 
     python tools/hdr_pattern.py [--hdr 54,108]
@@ -58,7 +59,8 @@ def main():
         print("buffer in uncached device memory", flush=True)
     nb = buf.numel() // args.region * args.region
     for hdr in [int(x) for x in args.hdr.split(",")]:
-        for pol, name in ((3, "read only"), (1, "nt"), (0, "plain"), (2, "write-through")):
+        for pol, name in ((3, "read only"), (1, "nt"), (0, "plain"), (2, "write-through"),
+                          (4, "plain coop"), (5, "write only")):
             ms = timed(lambda: mb.membw_hdr_tiles(buf.data_ptr(), buf.numel(), args.region, hdr,
                                                   pol, 13 * 1024, None))
             print(f"hdr tiles region {args.region} hdr {hdr:4d} B {name:14s}: {ms:7.3f} ms "

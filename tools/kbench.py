@@ -142,26 +142,28 @@ def main():
         n = 1 << 20
         copies = [zp.batch.generate("c2", n, device=dev) for _ in range(8)]
         rec = torch.empty((n, 8), dtype=torch.uint8, device=dev)
-        lib = zp._lib.hip()
         nbytes = int(copies[0][2].to(torch.int64).sum())
+        c2libs = libs or {"base": zp._lib.hip()}
         for label, order in (("warm (same copy)", [0] * 8), ("cold (8 rotating copies)",
                                                             list(range(8)))):
-            ms = []
-            for r in range(args.rounds):
-                s = torch.cuda.current_stream()
-                ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-                      for _ in order]
-                for (a, b), k in zip(ev, order):
-                    ar, of, ln = copies[k]
-                    a.record(s)
-                    lib.zp_parse_batch_device(ar.data_ptr(), of.data_ptr(), ln.data_ptr(), n,
-                                              rec.data_ptr(), None, None)
-                    b.record(s)
-                torch.cuda.synchronize()
-                ms += [a.elapsed_time(b) for a, b in ev]
-            med = float(np.median(ms))
-            print(f"c2 {label}: {med * 1e3:8.1f} us  {nbytes / med / 1e6:7.0f} GB/s  "
-                  f"{n / med / 1e3:8.0f} Mpkt/s", flush=True)
+            ms = {k: [] for k in c2libs}
+            for r in range(args.rounds):          # the libs interleaved by round
+                for name, lib in c2libs.items():
+                    s = torch.cuda.current_stream()
+                    ev = [(torch.cuda.Event(enable_timing=True),
+                           torch.cuda.Event(enable_timing=True)) for _ in order]
+                    for (a, b), k in zip(ev, order):
+                        ar, of, ln = copies[k]
+                        a.record(s)
+                        lib.zp_parse_batch_device(ar.data_ptr(), of.data_ptr(), ln.data_ptr(), n,
+                                                  rec.data_ptr(), None, None)
+                        b.record(s)
+                    torch.cuda.synchronize()
+                    ms[name] += [a.elapsed_time(b) for a, b in ev]
+            for name in c2libs:
+                med = float(np.median(ms[name]))
+                print(f"c2 {label} {name:>10s}: {med * 1e3:8.1f} us  {nbytes / med / 1e6:7.0f} GB/s  "
+                      f"{n / med / 1e3:8.0f} Mpkt/s", flush=True)
         del copies
         torch.cuda.empty_cache()
     for cfg in [c for c in args.configs.split(",") if c]:

@@ -356,7 +356,9 @@ extern "C" int membw_copy_gap(const void* src, void* dst, uint64_t bytes, int ga
 // every lane writes back the whole 64-B sectors covering bytes [f, f + hdr)
 // of its frame (f = its frame start: region/64 * lane, not 16-aligned), as
 // the builder's header write-back does. policy: 0 plain stores, 1
-// nontemporal, 2 write-through (sc1, system-coherent scope bit), 3 no write.
+// nontemporal, 2 write-through (sc1, system-coherent scope bit), 3 no write,
+// 4 plain stores by the whole wave (frame-major, coalesced), 5 plain stores
+// without the read.
 template <int POLICY>
 __global__ void __launch_bounds__(64) hdr_tiles(uint8_t* __restrict__ p, uint64_t region,
                                                 uint32_t hdr, uint32_t lds_bytes) {
@@ -367,7 +369,7 @@ __global__ void __launch_bounds__(64) hdr_tiles(uint8_t* __restrict__ p, uint64_
     uint8_t* base = p + w * region;
     const uint64_t nch = region / 16, items = (nch + 63) / 64;
     uint32_t acc = 0;
-    for (uint64_t i = 0; i < items; i += 8) {
+    for (uint64_t i = 0; i < (POLICY == 5 ? 0 : items); i += 8) {
         u32x4 v[8];
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
@@ -385,12 +387,25 @@ __global__ void __launch_bounds__(64) hdr_tiles(uint8_t* __restrict__ p, uint64_
         if (acc == 0x12345678u) base[0] = 1;
         return;
     }
+    u32x4 val = {acc, acc ^ 1u, acc ^ 2u, acc ^ 3u};
+    if (POLICY == 4) {
+        // wave-cooperative: the 64 frames' sector ranges as one linear list of
+        // 16-B chunks, consecutive lanes on consecutive chunks of a frame
+        const uint32_t cmax = ((hdr + 63) / 64 + 1) * 4;
+        for (uint32_t q = lane; q < 64 * cmax; q += 64) {
+            const uint64_t j = q / cmax, k = q % cmax;
+            const uint64_t fj = j * (region / 64);
+            const uint64_t a = (fj & ~63ull) + 16 * k, e = (fj + hdr + 63) & ~63ull;
+            if (a < e && a + 16 <= region)
+                *(__attribute__((address_space(1))) u32x4*)(base + a) = val;
+        }
+        return;
+    }
     const uint64_t f = (uint64_t)lane * (region / 64);
     const uint64_t s0 = f & ~63ull, s1 = (f + hdr + 63) & ~63ull;
-    u32x4 val = {acc, acc ^ 1u, acc ^ 2u, acc ^ 3u};
     for (uint64_t a = s0; a < s1 && a + 16 <= region; a += 16) {
         __attribute__((address_space(1))) u32x4* q = (__attribute__((address_space(1))) u32x4*)(base + a);
-        if (POLICY == 0) *q = val;
+        if (POLICY == 0 || POLICY == 5) *q = val;
         else if (POLICY == 1) __builtin_nontemporal_store(val, q);
         else __hip_atomic_store((__attribute__((address_space(1))) uint64_t*)q, ((uint64_t)val.y << 32) | val.x,
                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
@@ -408,6 +423,8 @@ extern "C" int membw_hdr_tiles(void* p, uint64_t bytes, uint64_t region, uint32_
     case 0: hipLaunchKernelGGL(hdr_tiles<0>, dim3((unsigned)nreg), dim3(64), lds_bytes, s, q, region, hdr, lds_bytes); break;
     case 1: hipLaunchKernelGGL(hdr_tiles<1>, dim3((unsigned)nreg), dim3(64), lds_bytes, s, q, region, hdr, lds_bytes); break;
     case 2: hipLaunchKernelGGL(hdr_tiles<2>, dim3((unsigned)nreg), dim3(64), lds_bytes, s, q, region, hdr, lds_bytes); break;
+    case 4: hipLaunchKernelGGL(hdr_tiles<4>, dim3((unsigned)nreg), dim3(64), lds_bytes, s, q, region, hdr, lds_bytes); break;
+    case 5: hipLaunchKernelGGL(hdr_tiles<5>, dim3((unsigned)nreg), dim3(64), lds_bytes, s, q, region, hdr, lds_bytes); break;
     default: hipLaunchKernelGGL(hdr_tiles<3>, dim3((unsigned)nreg), dim3(64), lds_bytes, s, q, region, hdr, lds_bytes); break;
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;
