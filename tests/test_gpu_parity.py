@@ -746,6 +746,75 @@ def test_parse_one_sizes(zp):
         lib.zp_ctx_destroy(ctx)
 
 
+def _v6_in_v6(outer_hbh, inner_hbh, l4="udp", tail=40, seed=0, valid=True):
+    """Ethernet + IPv6 (+ a 16-B Hop-by-Hop header) + IPv6 (+ a 16-B
+    Hop-by-Hop header) + UDP / ICMPv6 with its checksum over the inner
+    pseudo-header: the outer chain sits in front of an ip_in_ip header and
+    the inner one is an inner chain, so both keep their entries (ABI v6)."""
+    from pybuilder import internet_checksum, pseudo_header
+    rng = np.random.default_rng(seed)
+    proto = {"udp": 17, "icmpv6": 58}[l4]
+    f = bytearray(rng.integers(0, 256, 14 + 80 + 16 * (outer_hbh + inner_hbh) + tail,
+                               dtype=np.uint8).tobytes())
+    f[12:14] = b"\x86\xdd"
+    pos = 14
+    for k, hbh in enumerate((outer_hbh, inner_hbh)):
+        nxt = 41 if k == 0 else proto
+        f[pos] = 0x60
+        if hbh:
+            f[pos + 6] = 0                                  # Hop-by-Hop (headers.rs:90-113)
+            f[pos + 40] = nxt
+            f[pos + 41] = 1                                 # (1 + 1) * 8 = 16 B
+        else:
+            f[pos + 6] = nxt
+        ip = pos
+        pos += 40 + 16 * hbh
+    src, dst = f[ip + 8:ip + 24], f[ip + 24:ip + 40]
+    if l4 == "udp":
+        f[pos + 4:pos + 6] = tail.to_bytes(2, "big")        # length == slice (parser.rs:262)
+        ck = pos + 6
+    else:
+        f[pos] = 128                                        # echo request
+        ck = pos + 2
+    f[ck:ck + 2] = b"\0\0"
+    c = internet_checksum(f[pos:], pseudo_header(src, dst, proto, tail))
+    f[ck:ck + 2] = (c if valid else c ^ 0x0101).to_bytes(2, "big")
+    return bytes(f)
+
+
+def test_parse_one_chain_entries(zp):
+    """zp_parse_one on frames whose chains keep their entries (an outer chain
+    in front of ip_in_ip, an inner chain): the server stores the entries,
+    waits for them, then the record with its acknowledgement in one 16-B
+    store; both modes equal the oracle, entries included."""
+    import ctypes
+    R = zp.records
+    frames = [_v6_in_v6(o, i, l4, seed=s, valid=v)
+              for o in (0, 1) for i in (0, 1) for l4 in ("udp", "icmpv6")
+              for s, v in ((1, True), (2, False), (3, True))]
+    want = [orc.parse_one(f) for f in frames]
+    flags = [int(w[1]["flags"]) for w in want if w[0] == 0]
+    assert any(x & R.F_INNER_EXT for x in flags) and any(x & R.F_EXT for x in flags)
+    assert sum(1 for w in want if w[0]) >= 8
+    lib = zp._lib.hip()
+    ctx = lib.zp_ctx_create(0, 0)
+    try:
+        for idle in (5000, 0, 5000):
+            assert lib.zp_parse_one_config(ctx, idle) == 0
+            for rep in range(3):
+                for f, (err, wrec, wext) in zip(frames, want):
+                    rec = np.zeros(1, R.RECORD_DTYPE)
+                    ext = np.full((2, 16), 0xA5, np.uint8)
+                    buf = ctypes.create_string_buffer(f, len(f))
+                    rc = lib.zp_parse_one(ctx, ctypes.addressof(buf), len(f), rec.ctypes.data,
+                                          ext.ctypes.data)
+                    assert rc == err and rec.tobytes() == orc.pack(wrec, wext).tobytes(), \
+                        (idle, rep, len(f), rc, err)
+                    assert ext.tobytes() == wext.view(np.uint8).tobytes(), (idle, rep, len(f))
+    finally:
+        lib.zp_ctx_destroy(ctx)
+
+
 def test_parse_one_server_lifecycle(zp, golden):
     """The resident zp_parse_one server across its life cycle: a tiny idle
     timeout with random gaps between calls, so that the wave leaves between

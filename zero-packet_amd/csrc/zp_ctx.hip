@@ -72,7 +72,8 @@ struct zp_ctx {
 #define ONE_OFFS 8       // uint64_t: ONE_FRAME (launch mode)
 #define ONE_LENS 16      // uint32_t (launch mode)
 #define ONE_REC 64       // zp_record (8 B)
-#define ONE_ACK 80       // uint32_t: seq of the last finished request (server mode)
+#define ONE_ACK 72       // uint32_t: seq of the last finished request (server mode), written
+                         // with the record by one 16-B store
 #define ONE_EXT 96       // zp_ext_offsets[2]
 #define ONE_FRAME 128
 #define ONE_MAX (64u << 10)

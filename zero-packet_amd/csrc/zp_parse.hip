@@ -928,7 +928,8 @@ template <bool COLS, bool SYS = false>
 __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, WaveLds& lds,
                                             zp_record* __restrict__ records,
                                             zp_ext_offsets* __restrict__ ext,
-                                            const ColPtrs& cols, uintptr_t sysbase = 0) {
+                                            const ColPtrs& cols, uintptr_t sysbase = 0,
+                                            zp_u32x2* sys_rec = nullptr) {
     uint4* tail = &lds.win[ZP_WIN_CH * 64];
     const uint8_t* g = (const uint8_t*)s.ga;
 #ifdef ZP_STAMPS
@@ -1081,8 +1082,8 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
         __builtin_nontemporal_store(q.x ^ q.y, (uint32_t*)records + p);
 #else
         if (SYS) {
-            const zp_u32x2 q = zp_pack(rec);
-            st_sys8(records + p, ((uint64_t)q.y << 32) | q.x);
+            // the server stores it with its acknowledgement (one 16-B store)
+            *sys_rec = zp_pack(rec);
         } else {
             __builtin_nontemporal_store(zp_pack(rec), (zp_u32x2*)(records + p));
         }
@@ -1101,14 +1102,14 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
                    hi = rec.flags & ZP_F_INNER_EXT;
         const uint64_t mo = __ballot(ho), mi = __ballot(hi);
         if (SYS) {                                        // one frame: its own entries
-            if (ho) {
-                st_sys8(ext + p, ((uint64_t)w.outer.y << 32) | w.outer.x);
-                st_sys8((uint8_t*)(ext + p) + 8, ((uint64_t)w.outer.w << 32) | w.outer.z);
-            }
-            if (hi) {
-                st_sys8(ext + n + p, ((uint64_t)w.inner.y << 32) | w.inner.x);
-                st_sys8((uint8_t*)(ext + n + p) + 8, ((uint64_t)w.inner.w << 32) | w.inner.z);
-            }
+            if (ho) st_sys16(sysbase, (uintptr_t)(ext + p),
+                             zp_u32x4{w.outer.x, w.outer.y, w.outer.z, w.outer.w});
+            if (hi) st_sys16(sysbase, (uintptr_t)(ext + n + p),
+                             zp_u32x4{w.inner.x, w.inner.y, w.inner.z, w.inner.w});
+            // the entries are in host memory before the record and its
+            // acknowledgement go out (a store's completion is one host-link
+            // round trip: frames without entries skip it)
+            if (ho || hi) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         } else {
         if (mo && (ho || __builtin_popcountll(mo) >= ZP_EXT_DENSE))
             store_ext(ext, p, ho ? w.outer : make_uint4(0, 0, 0, 0));
@@ -1139,14 +1140,13 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
 #define ZP_KATTR_COLS __launch_bounds__(64 * ZP_WAVES)
 #endif
 // One streamed tile: descriptors given (len, ga), stream, walk, verdict,
-// record store. Shared by the batch kernels and the resident zp_parse_one
-// server below.
-template <bool COLS, bool TINY = !COLS, bool SYS = false>
+// record store (the batch kernels).
+template <bool COLS, bool TINY = !COLS>
 __device__ __forceinline__ void parse_tile(uint64_t t, uint32_t len, uintptr_t ga, uint64_t n,
                                            int lane, WaveLds& lds,
                                            zp_record* __restrict__ records,
                                            zp_ext_offsets* __restrict__ ext,
-                                           const ColPtrs& cols, uintptr_t sysbase = 0) {
+                                           const ColPtrs& cols) {
 #ifdef ZP_STAMPS
     const uint64_t wave_id = t;
 #endif
@@ -1162,7 +1162,6 @@ __device__ __forceinline__ void parse_tile(uint64_t t, uint32_t len, uintptr_t g
     TileState s;
     tile_setup(s, t, len, ga, n, lane, lds);
     STAMP(1);
-    OSTAMP(1);
     // stream: one group of ZP_G items per iteration (group 0 outside the
     // loop, so no load is in flight across the loop back-edge)
 #if ZP_SMALL_G
@@ -1171,16 +1170,15 @@ __device__ __forceinline__ void parse_tile(uint64_t t, uint32_t len, uintptr_t g
         // no dummy loads past the tile's end (c2 -8 %, c5 -1 %, c3/c4 0).
         uint4 vs[ZP_SMALL_G];
         uint32_t ks[ZP_SMALL_G];
-        issue_group<ZP_SMALL_G, false, SYS>(0, s.nitems, s.cur, s.R, lane, fallback, vs, ks, sysbase);
+        issue_group<ZP_SMALL_G>(0, s.nitems, s.cur, s.R, lane, fallback, vs, ks);
         STAMP(2);
-        OSTAMP(2);
         consume_group<ZP_SMALL_G>(0, s.nitems, lane, vs, ks, win, tail, lds.cend, s.run);
     } else
 #endif
     {
     uint4 va[ZP_G];
     uint32_t ka[ZP_G];
-    issue_group<ZP_G, false, SYS>(0, s.nitems, s.cur, s.R, lane, fallback, va, ka, sysbase);
+    issue_group<ZP_G>(0, s.nitems, s.cur, s.R, lane, fallback, va, ka);
     STAMP(2);
     consume_group<ZP_G>(0, s.nitems, lane, va, ka, win, tail, lds.cend, s.run);
     for (uint32_t i0 = ZP_G; i0 < s.nitems; i0 += ZP_G) {
@@ -1188,7 +1186,7 @@ __device__ __forceinline__ void parse_tile(uint64_t t, uint32_t len, uintptr_t g
         if (s.nitems - i0 <= 2) {                 // the last 1-2 items as a pair
             uint4 vt[2];
             uint32_t kt[2];
-            issue_group<2, false, SYS>(i0, s.nitems, s.cur, s.R, lane, fallback, vt, kt, sysbase);
+            issue_group<2>(i0, s.nitems, s.cur, s.R, lane, fallback, vt, kt);
             consume_group<2>(i0, s.nitems, lane, vt, kt, win, tail, lds.cend, s.run);
             break;
         }
@@ -1201,12 +1199,12 @@ __device__ __forceinline__ void parse_tile(uint64_t t, uint32_t len, uintptr_t g
         if (s.nitems - i0 <= ZP_TAIL_G) {
             uint4 vt[ZP_TAIL_G];
             uint32_t kt[ZP_TAIL_G];
-            issue_group<ZP_TAIL_G, false, SYS>(i0, s.nitems, s.cur, s.R, lane, fallback, vt, kt, sysbase);
+            issue_group<ZP_TAIL_G>(i0, s.nitems, s.cur, s.R, lane, fallback, vt, kt);
             consume_group<ZP_TAIL_G>(i0, s.nitems, lane, vt, kt, win, tail, lds.cend, s.run);
             break;
         }
 #endif
-        issue_group<ZP_G, false, SYS>(i0, s.nitems, s.cur, s.R, lane, fallback, va, ka, sysbase);
+        issue_group<ZP_G>(i0, s.nitems, s.cur, s.R, lane, fallback, va, ka);
         consume_group<ZP_G>(i0, s.nitems, lane, va, ka, win, tail, lds.cend, s.run);
     }
     }
@@ -1224,10 +1222,8 @@ __device__ __forceinline__ void parse_tile(uint64_t t, uint32_t len, uintptr_t g
     __builtin_amdgcn_s_setprio(0);             // walk at priority 0 ...
 #endif
     STAMP(3);
-    OSTAMP(3);
-    tile_finish<COLS, SYS>(s, n, lane, lds, records, ext, cols, sysbase);
+    tile_finish<COLS>(s, n, lane, lds, records, ext, cols);
     STAMP(4);
-    OSTAMP(4);
 }
 
 template <bool COLS>
@@ -1363,8 +1359,9 @@ extern "C" int zp_parse_batch_columns_device(const uint8_t* arena, const uint64_
 // both sides").
 // --------------------------------------------------------------------------
 #define ZP_ONE_BELL 0        // uint64_t: seq << 32 | frame length (host writes)
-#define ZP_ONE_REC 64        // zp_record (server writes)
-#define ZP_ONE_ACK 80        // uint32_t: seq of the last finished request (server writes)
+#define ZP_ONE_REC 64        // zp_record (server writes) ...
+#define ZP_ONE_ACK 72        // ... and right after it, in the same 16-B store, the uint32_t
+                             // seq of the last finished request
 #define ZP_ONE_EXT 96        // zp_ext_offsets[2] (server writes)
 #define ZP_ONE_FRAME 128     // the frame (host writes)
 #define ZP_ONE_STOP 0xFFFFFFFFu   // doorbell length: leave now
@@ -1379,7 +1376,7 @@ extern "C" int zp_parse_batch_columns_device(const uint8_t* arena, const uint64_
 // record store are tile_finish's. Frames <= 64 KiB (ONE_MAX).
 __device__ __forceinline__ void one_frame_tile(uint32_t len, uintptr_t ga, int lane, WaveLds& lds,
                                                zp_record* records, zp_ext_offsets* ext,
-                                               uintptr_t sysbase) {
+                                               uintptr_t sysbase, zp_u32x2* rec_out) {
     const ColPtrs none{};
     const uint32_t shift = (uint32_t)(ga & 15);
     const uint32_t nch = len >= 64 ? (len + shift + 15) >> 4 : 0u;   // as tile_setup
@@ -1417,7 +1414,7 @@ __device__ __forceinline__ void one_frame_tile(uint32_t len, uintptr_t ga, int l
     s.rank = (uint32_t)lane;
     s.nitems = 0;
     s.run = 0;
-    tile_finish<false, true>(s, 1, lane, lds, records, ext, none, sysbase);
+    tile_finish<false, true>(s, 1, lane, lds, records, ext, none, sysbase, rec_out);
 }
 
 __global__ void __launch_bounds__(64)
@@ -1460,22 +1457,14 @@ zp_one_server_kernel(uint8_t* blk, uint32_t seq, uint64_t idle) {
             // every load of the frame and every store of the results is
             // system-scope (SYS): nothing is left in a cache to invalidate
             // or write back
-#ifdef ZP_ONE_BATCH_TILE   // A/B: the batch kernel's tile path for the one frame
-            parse_tile<false, false, true>(0, lane == 0 ? blen : 0u, (uintptr_t)(blk + ZP_ONE_FRAME), 1,
-                                    lane, lds,
-                                    (zp_record*)(blk + ZP_ONE_REC),
-                                    (zp_ext_offsets*)(blk + ZP_ONE_EXT), none, (uintptr_t)blk);
-#else
+            zp_u32x2 rec{0u, 0u};
             one_frame_tile(blen, (uintptr_t)(blk + ZP_ONE_FRAME), lane, lds,
                            (zp_record*)(blk + ZP_ONE_REC), (zp_ext_offsets*)(blk + ZP_ONE_EXT),
-                           (uintptr_t)blk);
-#endif
+                           (uintptr_t)blk, &rec);
 #ifdef ZP_ONE_STAMPS
             const uint64_t t_tile = __builtin_amdgcn_s_memrealtime();
             const uint64_t c_tile = __builtin_amdgcn_s_memtime();
 #endif
-            // record + chains (system-scope stores) complete before the ack
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #ifdef ZP_ONE_STAMPS
             if (lane == 0) {
                 st_sys8(blk + 32, t_bell);
@@ -1487,9 +1476,12 @@ zp_one_server_kernel(uint8_t* blk, uint32_t seq, uint64_t idle) {
             polls = 0;
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
+            // The record and the acknowledgement in one 16-B store: the host
+            // sees both at once, so nothing waits for the record's completion
+            // first (a host-link round trip, ~1.2 us; the chain entries,
+            // when there are any, completed inside the tile).
             if (lane == 0)
-                __hip_atomic_store((uint32_t*)(blk + ZP_ONE_ACK), bseq, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_SYSTEM);
+                st_sys16((uintptr_t)blk, (uintptr_t)(blk + ZP_ONE_REC), zp_u32x4{rec.x, rec.y, bseq, 0u});
             wave_lds_fence();                                 // LDS reused by the next request
             last = __builtin_amdgcn_s_memrealtime();
         }

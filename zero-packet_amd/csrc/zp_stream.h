@@ -57,6 +57,13 @@ __device__ __forceinline__ uint4 ld_sys16(uintptr_t base, uintptr_t a) {
 __device__ __forceinline__ void st_sys8(void* p, uint64_t v) {
     __hip_atomic_store((ZP_GLOBAL uint64_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+// One 16-B write-through vector store at a (16-B aligned, inside the block):
+// a single write request, so the host sees its 16 bytes together.
+__device__ __forceinline__ void st_sys16(uintptr_t base, uintptr_t a, zp_u32x4 v) {
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)ZP_SYS_BYTES, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)(uint32_t)(a - base), 0, 1 | 16);   // sc0 sc1
+}
 
 // A readable 16-B chunk for masked lanes of frames that own no bytes.
 static __device__ uint4 zp_safe_chunk;
@@ -230,11 +237,10 @@ __device__ __forceinline__ void build_starts(uint32_t w0, const Cursor& c, const
 // Always issues exactly G loads (items past the end re-read the wave's last
 // chunk, or a dummy): a static load count keeps the compiler's s_waitcnt
 // exact.
-template <int G, bool T4 = false, bool SYS = false>
+template <int G, bool T4 = false>
 __device__ __forceinline__ void issue_group(uint32_t i0, uint32_t nitems, Cursor& c,
                                             const Ranked& R, int lane, uintptr_t fallback,
-                                            uint4 (&v)[G], uint32_t (&keep)[G],
-                                            uintptr_t sysbase = 0) {
+                                            uint4 (&v)[G], uint32_t (&keep)[G]) {
     uintptr_t a[G];
 #ifndef ZP_FMASK_ITEM
     // The G items' frame-start masks in one LDS round trip (G divides 64, so
@@ -295,15 +301,7 @@ __device__ __forceinline__ void issue_group(uint32_t i0, uint32_t nitems, Cursor
     }
 #ifndef ZP_ABL_STREAM_OFF
 #pragma unroll
-    for (int q = 0; q < G; ++q) {
-        // SYS: lanes past the frame's end and items past the tile load
-        // nothing (an offset past the buffer reads 0 without a memory
-        // access): system-scope loads of one address from many lanes are not
-        // merged, and the clamped duplicates cost ~0.1 us each over the host
-        // link (a 1.5 KB frame took 22 us with them)
-        v[q] = SYS ? ld_sys16(sysbase, (keep[q] & KEEP_IN) ? a[q] : sysbase + 0xFFFFFFF0u)
-                   : ld_stream(a[q]);
-    }
+    for (int q = 0; q < G; ++q) v[q] = ld_stream(a[q]);
 #endif
     // Compiler barrier: keeps LLVM from sinking the loads below the consume
     // of the previous group (which would serialise the double buffer).
