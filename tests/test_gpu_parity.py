@@ -815,6 +815,58 @@ def test_parse_one_chain_entries(zp):
         lib.zp_ctx_destroy(ctx)
 
 
+def _udp4(total, seed, valid=True):
+    """Ethernet + IPv4 (IHL 5) + UDP frame of `total` bytes, checksums valid
+    (or the UDP one off by one bit pair)."""
+    from pybuilder import internet_checksum, pseudo_header
+    rng = np.random.default_rng(seed)
+    f = bytearray(rng.integers(0, 256, total, dtype=np.uint8).tobytes())
+    f[12:14] = b"\x08\x00"
+    f[14:16] = b"\x45\x00"
+    f[16:18] = (total - 14).to_bytes(2, "big")
+    f[20:22] = b"\0\0"
+    f[23] = 17
+    f[24:26] = b"\0\0"
+    f[24:26] = internet_checksum(f[14:34]).to_bytes(2, "big")
+    f[38:40] = (total - 34).to_bytes(2, "big")
+    f[40:42] = b"\0\0"
+    c = internet_checksum(f[34:], pseudo_header(f[26:30], f[30:34], 17, total - 34))
+    f[40:42] = (c if valid else c ^ 0x0101).to_bytes(2, "big")
+    return bytes(f)
+
+
+def test_parse_one_lengths(zp):
+    """zp_parse_one at every length from 1,490 to 1,540 bytes (around the
+    Ethernet maximum) and at short ones, accepted and rejected, back to back
+    so that each request overwrites the previous one's bytes in the block;
+    both modes equal the oracle."""
+    import ctypes
+    R = zp.records
+    frames = [_udp4(L, L, valid=(L % 3 != 0)) for L in range(1490, 1541)]
+    frames += [_udp4(L, L) for L in (64, 65, 75, 76, 77, 100, 111, 112, 113, 127, 128, 129)]
+    frames += [bytes(f[:L]) for f, L in ((_udp4(200, 1), 40), (_udp4(200, 2), 63))]
+    want = [orc.parse_one(f) for f in frames]
+    assert sum(1 for w in want if w[0] == 0) > 30 and sum(1 for w in want if w[0]) > 15
+    lib = zp._lib.hip()
+    ctx = lib.zp_ctx_create(0, 0)
+    rng = np.random.default_rng(3)
+    try:
+        for idle in (5000, 0):
+            assert lib.zp_parse_one_config(ctx, idle) == 0
+            for i in list(range(len(frames))) + list(rng.integers(0, len(frames), 300)):
+                f, (err, wrec, wext) = frames[i], want[i]
+                rec = np.zeros(1, R.RECORD_DTYPE)
+                ext = np.full((2, 16), 0xA5, np.uint8)
+                buf = ctypes.create_string_buffer(f, max(len(f), 1))
+                rc = lib.zp_parse_one(ctx, ctypes.addressof(buf), len(f), rec.ctypes.data,
+                                      ext.ctypes.data)
+                assert rc == err and rec.tobytes() == orc.pack(wrec, wext).tobytes(), \
+                    (idle, len(f), rc, err)
+                assert ext.tobytes() == wext.view(np.uint8).tobytes(), (idle, len(f))
+    finally:
+        lib.zp_ctx_destroy(ctx)
+
+
 def test_parse_one_server_lifecycle(zp, golden):
     """The resident zp_parse_one server across its life cycle: a tiny idle
     timeout with random gaps between calls, so that the wave leaves between
