@@ -1218,7 +1218,9 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
             results[i] = r;
         }
     }
+#if !(ZB_OP_PREFETCH && ZB_OP_KINDS && ZB_LANE_PAY)
     const OpGlobal og{ops + o0};
+#endif
     // ph: the wave copy moves the whole payload (ZB_PAY_HDR), unless it
     // overwrites the L4 header's own fields (a TCP data offset below 5: the
     // chain keeps the reference's write order then)
