@@ -1421,7 +1421,6 @@ __global__ void __launch_bounds__(64)
 zp_one_server_kernel(uint8_t* blk, uint32_t seq, uint64_t idle) {
     __shared__ WaveLds lds;
     const int lane = threadIdx.x & 63;
-    const ColPtrs none{};
 #ifdef ZP_ONE_STAMPS   // diagnostic build only (tools/parse_one_latency.py --lib)
     uint64_t polls = 0;
 #endif
