@@ -51,7 +51,8 @@ int main() {
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
     uint64_t* d = nullptr;
     if (hipMalloc(&d, 16ull * cus * 40) != hipSuccess) return 1;
-    probe<0, 1>(d, cus); probe<4096, 1>(d, cus); probe<8192, 1>(d, cus); probe<8960, 1>(d, cus);
+    probe<0, 1>(d, cus); probe<4096, 1>(d, cus); probe<7168, 1>(d, cus); probe<7680, 1>(d, cus);
+    probe<7936, 1>(d, cus); probe<8064, 1>(d, cus); probe<8192, 1>(d, cus); probe<8960, 1>(d, cus);
     probe<9216, 1>(d, cus);
     probe<0, 2>(d, cus); probe<8192, 2>(d, cus); probe<8960, 2>(d, cus);
     probe<8192, 4>(d, cus); probe<8960, 4>(d, cus);
