@@ -924,14 +924,18 @@ __device__ __forceinline__ void store_ext(zp_ext_offsets* base, uint64_t i, uint
 
 // Header walk + checksum verdict + record store of a streamed tile; with COLS
 // also the column views, from the same LDS window (no second pass).
-template <bool COLS, bool SYS = false>
-__device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, WaveLds& lds,
+template <bool COLS, bool SYS = false, class L = WaveLds>
+__device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, L& lds,
                                             zp_record* __restrict__ records,
                                             zp_ext_offsets* __restrict__ ext,
                                             const ColPtrs& cols, uintptr_t sysbase = 0,
                                             zp_u32x2* sys_rec = nullptr) {
-    uint4* tail = &lds.win[ZP_WIN_CH * 64];
+    constexpr bool TAILS = sizeof(lds.win) > sizeof(uint4) * ZP_WIN_CH * 64;   // last-chunk cells
+    static_assert(TAILS || (ZP_REGION && !SYS), "the tail-free layout needs the region path");
+    uint4* tail = TAILS ? &lds.win[0] + ZP_WIN_CH * 64 : nullptr;
     const uint8_t* g = (const uint8_t*)s.ga;
+    // the frame's stream sum (before the regions overlay the running sums)
+    const uint32_t fsum = lds.cend[s.rank & 63u] - ((s.rank & 63u) ? lds.cend[(s.rank & 63u) - 1u] : 0u);
 #ifdef ZP_STAMPS
     const uint64_t wave_id = s.tile;
 #endif
@@ -956,12 +960,27 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
         mytail = tail[s.rank & 63u];
         fv.reg = nullptr;
     } else {
-        static_assert(64 * ZP_RSTRIDE * 4 <= (ZP_WIN_CH + 1) * 64 * 16, "regions fit the window LDS");
+        static_assert(64 * ZP_RSTRIDE * 4 <= sizeof(L), "regions fit the wave's LDS");
         const uint32_t rk = s.rank & 63u;
         uint4 cell[ZP_WIN_CH];
 #pragma unroll
         for (uint32_t c = 0; c < ZP_WIN_CH; ++c) cell[c] = lds.win[c * 64 + ((rk ^ c) & 63u)];
-        mytail = tail[rk];
+        if (TAILS) {
+            mytail = tail[rk];
+        } else {
+            // The bytes past the frame's end in its last chunk: the next
+            // rank's first window cell when that is the same 16-B chunk
+            // (frames back to back), else the chunk from memory (the tile's
+            // last frame, gaps, other orders).
+            const uint32_t nr = (rk + 1u) & 63u;
+            const uint4 ncell = lds.win[nr];                   // chunk 0 of rank rk + 1
+            const uintptr_t nA = ((((uintptr_t)bperm(s.R.org_hi, nr)) << 32) | bperm(s.R.org_lo, nr)) +
+                                 16ull * bperm(s.R.pfx, nr);
+            const uintptr_t lastc = (s.ga + s.len - 1u) & ~(uintptr_t)15;
+            const bool nxt = rk + 1u < s.cur.nz && nA == lastc;
+            const bool need = s.live && s.len >= 64 && !s.giant && ((s.len + s.shift) & 15u) != 0u;
+            mytail = nxt ? ncell : (need ? ldg16(lastc) : make_uint4(0, 0, 0, 0));
+        }
         wave_lds_fence();
         uint32_t* reg = (uint32_t*)&lds.win[0] + (uint32_t)lane * ZP_RSTRIDE;
 #pragma unroll
@@ -1038,13 +1057,11 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
             ok = csum_ok_exact(g, w.l4, s.len, w.acc);
         } else {
             const bool odd = (s.ga + w.l4) & 1;
-            const uint32_t r = s.rank;
-            const uint32_t fsum = lds.cend[r] - (r ? lds.cend[r - 1] : 0u);
             const uint32_t he = (s.len + s.shift) & 15u;    // bytes of the last chunk in use
 #if ZP_REGION
             const uint32_t ex = he ? range_sum(mytail, he, 16u) : 0u;
 #else
-            const uint32_t ex = he ? range_sum(tail[r], he, 16u) : 0u;
+            const uint32_t ex = he ? range_sum(tail[s.rank], he, 16u) : 0u;
 #endif
 #ifdef ZP_ABL_NO_L4HDR
             ok = csum_ok(w.acc, fsum - ex, odd);                  // timing ablation only
@@ -1141,9 +1158,9 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
 #endif
 // One streamed tile: descriptors given (len, ga), stream, walk, verdict,
 // record store (the batch kernels).
-template <bool COLS, bool TINY = !COLS>
+template <bool COLS, bool TINY = !COLS, class L = WaveLdsParse>
 __device__ __forceinline__ void parse_tile(uint64_t t, uint32_t len, uintptr_t ga, uint64_t n,
-                                           int lane, WaveLds& lds,
+                                           int lane, L& lds,
                                            zp_record* __restrict__ records,
                                            zp_ext_offsets* __restrict__ ext,
                                            const ColPtrs& cols) {
@@ -1152,7 +1169,8 @@ __device__ __forceinline__ void parse_tile(uint64_t t, uint32_t len, uintptr_t g
 #endif
     const uintptr_t fallback = (uintptr_t)&zp_safe_chunk;   // dummy loads when T == 0
     uint4* win = &lds.win[0];
-    uint4* tail = &lds.win[ZP_WIN_CH * 64];
+    uint4* tail = sizeof(lds.win) > sizeof(uint4) * ZP_WIN_CH * 64 ? &lds.win[0] + ZP_WIN_CH * 64
+                                                                  : nullptr;
 #if ZP_TINY
     // a tile of 64-B frames: registers only (wave-uniform test)
     if (TINY && !__ballot(t * 64 + lane < n && len != 64u) &&
@@ -1222,7 +1240,7 @@ __device__ __forceinline__ void parse_tile(uint64_t t, uint32_t len, uintptr_t g
     __builtin_amdgcn_s_setprio(0);             // walk at priority 0 ...
 #endif
     STAMP(3);
-    tile_finish<COLS>(s, n, lane, lds, records, ext, cols);
+    tile_finish<COLS, false, L>(s, n, lane, lds, records, ext, cols);
     STAMP(4);
 }
 
@@ -1233,10 +1251,10 @@ __device__ __forceinline__ void parse_tiles(const uint8_t* __restrict__ arena,
                                             zp_record* __restrict__ records,
                                             zp_ext_offsets* __restrict__ ext,
                                             const ColPtrs& cols) {
-    __shared__ WaveLds lds_all[ZP_WAVES];
+    __shared__ WaveLdsParse lds_all[ZP_WAVES];
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
-    WaveLds& lds = lds_all[wid];
+    WaveLdsParse& lds = lds_all[wid];
     // ZP_K consecutive tiles per wave (one contiguous band of the arena)
 #ifdef ZP_SEG
     // A/B: the grid's blocks interleaved over ZP_SEG contiguous segments of the

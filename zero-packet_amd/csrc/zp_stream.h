@@ -188,7 +188,7 @@ __device__ __forceinline__ uint32_t range_sum(uint4 v, uint32_t lo, uint32_t hi)
 struct Cursor {          // wave-uniform
     uint32_t rbase;      // rank of the frame holding the chunk before the item
     uint32_t nz;         // number of ranks (frames that own chunks)
-    uint64_t* starts;    // LDS: starts[i & 63] = bit b set <=> a frame starts at 64i + b
+    uint64_t* starts;    // LDS: starts[i % ZP_STARTS] = bit b set <=> a frame starts at 64i + b
 };
 
 struct Ranked {          // lane r = frame of rank r
@@ -216,17 +216,20 @@ __device__ __forceinline__ uint32_t bperm(uint32_t v, uint32_t r) {
     return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(r << 2), (int)v);
 }
 
-// Rebuilds the start masks of items [w0, w0 + 64): one LDS atomic OR per
+#ifndef ZP_STARTS
+#define ZP_STARTS 64           // items per rebuild of the frame-start masks (a power of two >= ZP_G)
+#endif
+// Rebuilds the start masks of items [w0, w0 + ZP_STARTS): one LDS atomic OR per
 // frame starting there. Straight-line code (no loop): a loop here would make
 // LLVM's wait-count insertion drain the group in flight (vmcnt(0)).
 __device__ __forceinline__ void build_starts(uint32_t w0, const Cursor& c, const Ranked& R,
                                              int lane) {
-    c.starts[lane] = 0;
+    if ((uint32_t)lane < (uint32_t)ZP_STARTS) c.starts[lane] = 0;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const uint32_t it = R.pfx >> 6;
-    if ((uint32_t)lane < c.nz && it >= w0 && it < w0 + 64u)
+    if ((uint32_t)lane < c.nz && it >= w0 && it < w0 + (uint32_t)ZP_STARTS)
         __hip_atomic_fetch_or(&c.starts[it - w0], 1ull << (R.pfx & 63u), __ATOMIC_RELAXED,
                               __HIP_MEMORY_SCOPE_WAVEFRONT);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -245,12 +248,13 @@ __device__ __forceinline__ void issue_group(uint32_t i0, uint32_t nitems, Cursor
 #ifndef ZP_FMASK_ITEM
     // The G items' frame-start masks in one LDS round trip (G divides 64, so
     // the group never straddles a rebuild of the mask table).
-    static_assert(64 % G == 0 && G % 2 == 0, "group size must be even and divide 64");
-    if ((i0 & 63u) == 0 && i0 < nitems) build_starts(i0, c, R, lane);   // wave-uniform
+    static_assert(ZP_STARTS % G == 0 && G % 2 == 0 && ZP_STARTS <= 64,
+                  "group size must be even and divide ZP_STARTS");
+    if ((i0 & (ZP_STARTS - 1u)) == 0 && i0 < nitems) build_starts(i0, c, R, lane);   // wave-uniform
     // G/2 ds_read_b128 issued back to back, then one wait
     uint64_t Fq[G];
     zp_u32x4 m[G / 2];
-    const zp_u32x4* sp = (const zp_u32x4*)&c.starts[i0 & 63u];
+    const zp_u32x4* sp = (const zp_u32x4*)&c.starts[i0 & (ZP_STARTS - 1u)];
 #pragma unroll
     for (int q = 0; q < G / 2; ++q) m[q] = sp[q];
 #pragma unroll
@@ -268,10 +272,10 @@ __device__ __forceinline__ void issue_group(uint32_t i0, uint32_t nitems, Cursor
         const uint32_t i = i0 + q;
         const uint32_t base = 64u * i;
 #ifdef ZP_FMASK_ITEM
-        if ((i & 63u) == 0 && i < nitems) build_starts(i, c, R, lane);   // wave-uniform
+        if ((i & (ZP_STARTS - 1u)) == 0 && i < nitems) build_starts(i, c, R, lane);   // wave-uniform
         uint64_t F = 0;
         if (i < nitems) {
-            const uint64_t f = c.starts[i & 63u];
+            const uint64_t f = c.starts[i & (ZP_STARTS - 1u)];
             F = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(f >> 32)) << 32) |
                 (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)f);
         }
@@ -348,7 +352,7 @@ __device__ __forceinline__ void consume_group(uint32_t i0, uint32_t nitems, int 
         for (int x = 0; x < ZP_ABL_EXTRA; ++x) asm volatile("v_add_u32 %0, %0, 1" : "+v"(part));
 #endif
         if (k & KEEP_TAIL) {
-            tail[KEEP_RANK(k)] = v[q];
+            if (tail != nullptr) tail[KEEP_RANK(k)] = v[q];
             cend[KEEP_RANK(k)] = run + P;
         }
         // T4 streams: the running sum through the marked byte of a frame
@@ -365,11 +369,25 @@ __device__ __forceinline__ void consume_group(uint32_t i0, uint32_t nitems, int 
 // The batch kernel.
 // --------------------------------------------------------------------------
 // One tile = 64 consecutive frames on one wave (lane = frame).
-struct WaveLds {
-    uint4 win[(ZP_WIN_CH + 1) * 64];   // header windows [ZP_WIN_CH][64] + last chunks [64]
-    uint32_t cend[64];                  // running stream sum at each frame's last chunk
-    uint64_t starts[64];                // per-item frame-start masks
+template <int TAILS>
+struct WaveLdsT {
+    uint4 win[(ZP_WIN_CH + TAILS) * 64];   // header windows [ZP_WIN_CH][64] (+ last chunks [64])
+    uint32_t cend[64];                      // running stream sum at each frame's last chunk
+    uint64_t starts[ZP_STARTS];             // per-item frame-start masks
 };
+// With the last chunk of every frame (the builder, the zp_parse_one server).
+typedef WaveLdsT<1> WaveLds;
+// The parse kernels' layout. ZP_NO_TAIL (A/B, with ZP_STARTS 32): no
+// last-chunk cells; the bytes past a frame's end come from the next rank's
+// first window cell (the same 16-B chunk when frames lie back to back) or
+// from memory, so a wave needs 7.5 KiB and a CU holds 21 waves instead of 18
+// (profiles/r05_lds_residency.log). Byte-exact (GPU suite green with it) but
+// within +-1 % on every config on two boxes
+// (profiles/r05_kbench_tail_free_layout.log): off.
+#ifndef ZP_NO_TAIL
+#define ZP_NO_TAIL 0
+#endif
+typedef WaveLdsT<ZP_NO_TAIL ? 0 : 1> WaveLdsParse;
 
 struct TileState {
     uint64_t tile;
@@ -377,6 +395,7 @@ struct TileState {
     uint32_t len, shift, wlen, rank;
     bool live, giant;
     uint32_t nitems;         // wave-uniform
+    uint64_t ranked;         // wave-uniform: lanes whose frames own chunks (rank order = lane order)
     Ranked R;
     Cursor cur;
     uint32_t run;            // running stream sum
@@ -384,8 +403,9 @@ struct TileState {
 
 // Chunk ranges, ranks and the compacted per-rank frame table of a tile.
 // len = 0 lanes (past the batch) own no chunks.
+template <class L>
 __device__ __forceinline__ void tile_setup(TileState& s, uint64_t tile, uint32_t len,
-                                           uintptr_t ga, uint64_t n, int lane, WaveLds& lds,
+                                           uintptr_t ga, uint64_t n, int lane, L& lds,
                                            bool win_only = false, uint32_t mark = ~0u) {
     s.tile = tile;
     s.ga = ga;
@@ -401,6 +421,7 @@ __device__ __forceinline__ void tile_setup(TileState& s, uint64_t tile, uint32_t
                                                                           : len + s.shift;
     const uint32_t nch = len >= 64 ? (span + 15) >> 4 : 0u;
     const uint64_t M = __ballot(nch > 0);
+    s.ranked = M;
     s.rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(M >> 32),
                                        __builtin_amdgcn_mbcnt_lo((uint32_t)M, 0u));
     const uint32_t incl = wave_scan(nch);
