@@ -42,6 +42,9 @@ def main():
     ap.add_argument("--hdr", default="54,108")
     ap.add_argument("--region", type=int, default=50016, help="tile bytes (c3: 64 x 781.5 B)")
     ap.add_argument("--gib", type=int, default=3, help="buffer (4M c3 frames = 3.28 GB)")
+    ap.add_argument("--twophase", action="store_true",
+                    help="also the write-back in two kernels: reads + a contiguous 64-B slot per "
+                         "frame, then the slots read back and the sectors written")
     ap.add_argument("--uncached", action="store_true",
                     help="the buffer in uncached device memory (tools/ucmem.py)")
     args = ap.parse_args()
@@ -65,6 +68,18 @@ def main():
                                                   pol, 13 * 1024, None))
             print(f"hdr tiles region {args.region} hdr {hdr:4d} B {name:14s}: {ms:7.3f} ms "
                   f"read {nb / ms / 1e6:6.0f} GB/s", flush=True)
+    if args.twophase:
+        mb.membw_hdr_twophase.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+                                          ctypes.c_uint32, ctypes.c_void_p, ctypes.c_int,
+                                          ctypes.c_void_p]
+        tmp = torch.empty(nb // args.region * 4096, dtype=torch.uint8, device=d)
+        for hdr in [int(x) for x in args.hdr.split(",")]:
+            for ph, name in ((3, "two phases"), (1, "phase 1 only"), (2, "phase 2 only")):
+                ms = timed(lambda: mb.membw_hdr_twophase(buf.data_ptr(), buf.numel(), args.region,
+                                                         hdr, tmp.data_ptr(), ph, None))
+                print(f"hdr tiles region {args.region} hdr {hdr:4d} B {name:14s}: {ms:7.3f} ms",
+                      flush=True)
+        del tmp
     zp = importlib.import_module("zero-packet_amd")
     n = 1 << 22
     arena, offs, lens = zp.batch.generate("c3", n, device=d)

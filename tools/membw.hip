@@ -414,6 +414,57 @@ __global__ void __launch_bounds__(64) hdr_tiles(uint8_t* __restrict__ p, uint64_
     }
 }
 
+// The same header write-back in two phases (a builder that keeps its reads
+// and its scattered writes apart in time): kernel 1 reads the tiles and
+// writes each frame's 64-B header slot to a contiguous temp buffer; kernel 2
+// reads the temp buffer and writes the whole 64-B sectors covering each
+// frame's first `hdr` bytes (plain stores).
+__global__ void __launch_bounds__(64) hdr_phase1(const uint8_t* __restrict__ p, uint64_t region,
+                                                 uint8_t* __restrict__ tmp) {
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    const int lane = threadIdx.x;
+    const uint64_t w = blockIdx.x;
+    const uint8_t* base = p + w * region;
+    const uint64_t nch = region / 16, items = (nch + 63) / 64;
+    uint32_t acc = 0;
+    for (uint64_t i = 0; i < items; i += 8) {
+        u32x4 v[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            uint64_t c = (i + q) * 64 + lane;
+            c = c < nch ? c : nch - 1;
+            v[q] = __builtin_nontemporal_load((const __attribute__((address_space(1))) u32x4*)(base + c * 16));
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc += v[q].x ^ v[q].y ^ v[q].z ^ v[q].w;
+    }
+    u32x4 val = {acc, acc ^ 1u, acc ^ 2u, acc ^ 3u};
+    __attribute__((address_space(1))) u32x4* t = (__attribute__((address_space(1))) u32x4*)(tmp + w * 4096);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) t[k * 64 + lane] = val;          // 4 KiB per tile, coalesced
+}
+__global__ void __launch_bounds__(64) hdr_phase2(uint8_t* __restrict__ p, uint64_t region, uint32_t hdr,
+                                                 const uint8_t* __restrict__ tmp) {
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    const int lane = threadIdx.x;
+    const uint64_t w = blockIdx.x;
+    uint8_t* base = p + w * region;
+    const __attribute__((address_space(1))) u32x4* t = (const __attribute__((address_space(1))) u32x4*)(tmp + w * 4096);
+    u32x4 val = t[lane] ^ t[64 + lane] ^ t[128 + lane] ^ t[192 + lane];
+    const uint64_t f = (uint64_t)lane * (region / 64);
+    const uint64_t s0 = f & ~63ull, s1 = (f + hdr + 63) & ~63ull;
+    for (uint64_t a = s0; a < s1 && a + 16 <= region; a += 16)
+        *(__attribute__((address_space(1))) u32x4*)(base + a) = val;
+}
+extern "C" int membw_hdr_twophase(void* p, uint64_t bytes, uint64_t region, uint32_t hdr, void* tmp,
+                                  int phases, void* stream) {
+    const uint64_t nreg = bytes / region;
+    hipStream_t s = (hipStream_t)stream;
+    if (phases & 1) hipLaunchKernelGGL(hdr_phase1, dim3((unsigned)nreg), dim3(64), 0, s, (const uint8_t*)p, region, (uint8_t*)tmp);
+    if (phases & 2) hipLaunchKernelGGL(hdr_phase2, dim3((unsigned)nreg), dim3(64), 0, s, (uint8_t*)p, region, hdr, (const uint8_t*)tmp);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 extern "C" int membw_hdr_tiles(void* p, uint64_t bytes, uint64_t region, uint32_t hdr, int policy,
                                uint32_t lds_bytes, void* stream) {
     const uint64_t nreg = bytes / region;
