@@ -24,11 +24,16 @@ def main():
                 [ctypes.c_void_p] * 3
             lib.zp_dbg_fb_count.restype = ctypes.c_ulonglong
             lib.zp_dbg_fb_count()
+            rep = getattr(lib, "zp_dbg_fb_repeat", None)
+            if rep is not None:
+                rep.restype = ctypes.c_ulonglong
+                rep()
             lib.zp_parse_batch_device(arena.data_ptr(), offs.data_ptr(), lens.data_ptr(), n,
                                       rec.data_ptr(), ext.data_ptr(), None)
             torch.cuda.synchronize()
             c = lib.zp_dbg_fb_count()
-            print(f"{cfg} {v}: {c} fallback chunk loads, {c / n:.3f} per frame", flush=True)
+            r = f", {rep()} of them repeats of a chunk the frame had loaded" if rep is not None else ""
+            print(f"{cfg} {v}: {c} fallback chunk loads, {c / n:.3f} per frame{r}", flush=True)
 
 
 if __name__ == "__main__":

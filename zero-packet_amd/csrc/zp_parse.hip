@@ -181,6 +181,9 @@ struct FrameView {
 #ifdef ZP_FB2
     uint4 xc2;               // A/B: and the chunk after it
 #endif
+#ifdef ZP_DBG_FBCOUNT
+    uint64_t seen = 0;       // diagnostics: past-window chunks (< 64) loaded so far
+#endif
 };
 
 __device__ __forceinline__ uint4 win_chunk(const FrameView& f, uint32_t c) {
@@ -206,11 +209,18 @@ __device__ __forceinline__ uint32_t win_dw(const FrameView& f, uint32_t d) {
 // (deep IPv6 extension chains and IP-in-IP read a few bytes each from the
 // same chunks).
 #ifdef ZP_DBG_FBCOUNT   // diagnostic build only (tools/fbcount.py): fallback chunk loads
-__device__ unsigned long long zp_fb_count;
+__device__ unsigned long long zp_fb_count, zp_fb_repeat;
 extern "C" unsigned long long zp_dbg_fb_count(void) {
     unsigned long long v = 0, z = 0;
     (void)hipMemcpyFromSymbol(&v, HIP_SYMBOL(zp_fb_count), sizeof v);
     (void)hipMemcpyToSymbol(HIP_SYMBOL(zp_fb_count), &z, sizeof z);
+    return v;
+}
+// ... of which loads of a chunk this frame's walk had loaded before
+extern "C" unsigned long long zp_dbg_fb_repeat(void) {
+    unsigned long long v = 0, z = 0;
+    (void)hipMemcpyFromSymbol(&v, HIP_SYMBOL(zp_fb_repeat), sizeof v);
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(zp_fb_repeat), &z, sizeof z);
     return v;
 }
 #endif
@@ -229,6 +239,8 @@ __device__ __forceinline__ uint4 fb_chunk(FrameView& f, uint32_t c) {
     if (c != f.xi) {
 #ifdef ZP_DBG_FBCOUNT
         atomicAdd(&zp_fb_count, 1ull);
+        if (c < 64 && ((f.seen >> c) & 1ull)) atomicAdd(&zp_fb_repeat, 1ull);
+        if (c < 64) f.seen |= 1ull << c;
 #endif
         const uintptr_t a = ((uintptr_t)f.g & ~(uintptr_t)15) + 16u * c;
         f.xc = f.sysbase ? ld_sys16(f.sysbase, a) : ldg16(a);
