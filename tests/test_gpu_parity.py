@@ -867,6 +867,29 @@ def test_parse_one_lengths(zp):
         lib.zp_ctx_destroy(ctx)
 
 
+def test_parse_one_quiesce(zp, golden):
+    """PacketParser.parse through the default context's server, quiesce()
+    stopping it (the stream of the server wave is then idle, so a device-wide
+    synchronisation returns at once), and the next parse relaunching it; the
+    results equal the oracle's before and after."""
+    import time
+    import torch
+    frames = [bytes.fromhex(fx["bytes"]) for fx in golden["fixtures"]]
+
+    def result(f):
+        try:
+            return zp.parser.PacketParser.parse(f).debug()
+        except zp.parser.ZeroPacketError as e:
+            return repr(e)
+    want = [result(f) for f in frames]
+    for rep in range(3):
+        zp.parser.quiesce()
+        t0 = time.perf_counter()
+        torch.cuda.synchronize()
+        assert time.perf_counter() - t0 < 0.5
+        assert [result(f) for f in frames] == want, rep
+
+
 def test_parse_one_server_lifecycle(zp, golden):
     """The resident zp_parse_one server across its life cycle: a tiny idle
     timeout with random gaps between calls, so that the wave leaves between
