@@ -183,3 +183,32 @@ def test_gpu_columns_vs_oracle(zp, golden, case):
         for name in ("tcp_seq", "vlan_tci"):
             assert np.array_equal(fsub[name].cpu().numpy(), want[name]), mode
     assert zp.columns.auto_choice(a, o.numel(), zp.columns.NAMES) in ("fused", "split")
+
+
+@pytest.mark.gpu
+def test_parse_with_columns_fresh_arenas(zp):
+    """A caller that hands parse_with_columns(mode="auto") a fresh arena per
+    batch: the first four arenas of a shape are timed; once they agree, later
+    arenas of that shape take the agreed path without timing again, and the
+    remembered workloads stay bounded. Results equal the fused path's."""
+    import torch
+    d = torch.device("cuda:0")
+    C = zp.columns
+    C.reset_auto()
+    a0, o, l_ = zp.batch.generate("c5", 1 << 16, first=5, device=d)
+    names = ["src_addr", "dest_addr", "src_port", "dest_port", "protocol"]
+    want_r, _, want_c = C.parse_with_columns(a0, o, l_, names=names, mode="fused")
+    keep = []
+    t0 = C.auto_timings
+    for k in range(7):
+        a = a0.clone()                                  # a fresh buffer each batch
+        keep.append(a)
+        r, _, c = C.parse_with_columns(a, o, l_, names=names)
+        torch.cuda.synchronize()
+        assert torch.equal(r, want_r) and all(torch.equal(c[x], want_c[x]) for x in names), k
+    shape = next(iter(C._agree))
+    seen = C._agree[shape]
+    if len(set(seen[:4])) == 1:                         # the usual case: one path clearly faster
+        assert C.auto_timings - t0 == 4, seen
+    assert len(C._auto) <= C._AUTO_MAX
+    C.reset_auto()

@@ -8,6 +8,7 @@ downstream consumer (flow table, filter, sampler) needs no host pass. Column
 semantics and the reference getters they follow: include/zero_packet.h
 (zp_col). Entry i is 0 when record i holds an error or the reader is absent.
 """
+import collections
 import ctypes
 
 import numpy as np
@@ -80,7 +81,11 @@ def extract(arena, offs, lens, records, names=None, out=None, stream=None, check
 # columns +2-5 % fused; c4/c5/c6 -11 to -23 %). The library
 # times both paths on the first call of a workload and keeps the faster one.
 _AUTO_REPS = 2             # timed back-to-back runs per path (after one warm-up run)
-_auto = {}
+_AUTO_MAX = 256            # workload keys remembered (least recently used dropped)
+_AUTO_AGREE = 4            # arenas of one (device, columns, size octave) whose timings agree
+_auto = collections.OrderedDict()
+_agree = {}                # (device, columns, octave) -> the choices timed so far
+auto_timings = 0           # first calls that timed both paths (diagnostics, tests)
 
 
 def _auto_key(arena, n, names):
@@ -94,6 +99,14 @@ def reset_auto():
     a reused arena changed shape): the next call of each workload times both
     paths again."""
     _auto.clear()
+    _agree.clear()
+
+
+def _remember(key, choice):
+    _auto[key] = choice
+    _auto.move_to_end(key)
+    while len(_auto) > _AUTO_MAX:
+        _auto.popitem(last=False)
 
 
 def auto_choice(arena, n, names):
@@ -153,6 +166,18 @@ def parse_with_columns(arena, offs, lens, names=None, records=None, ext=None, ou
         return records, ext, {k: out[k] for k in names}
     key = _auto_key(arena, n, names)
     choice = _auto.get(key)
+    shape = (key[0],) + key[2:]
+    if choice is None and n:
+        # A caller that hands over a fresh arena per batch: once the first
+        # _AUTO_AGREE arenas of this shape agreed, new ones take that path
+        # without timing it again.
+        seen = _agree.get(shape, [])
+        if len(seen) >= _AUTO_AGREE and len(set(seen)) == 1:
+            choice = seen[0]
+            _remember(key, choice)
+    else:
+        if choice is not None:
+            _auto.move_to_end(key)
     if choice is None and n:
         # First call of this workload: each path once to warm up, then twice
         # back to back between two events (as a stream of calls runs), and
@@ -169,7 +194,13 @@ def parse_with_columns(arena, offs, lens, names=None, records=None, ext=None, ou
             b.record(ts)
             b.synchronize()
             ms[k] = a.elapsed_time(b)
-        choice = _auto[key] = min(ms, key=ms.get)
+        global auto_timings
+        auto_timings += 1
+        choice = min(ms, key=ms.get)
+        _remember(key, choice)
+        _agree.setdefault(shape, []).append(choice)
+        if len(_agree[shape]) > 64:
+            del _agree[shape][:-64]
         return records, ext, {k: out[k] for k in names}
     paths[choice or "fused"]()
     return records, ext, {k: out[k] for k in names}
