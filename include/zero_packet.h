@@ -331,11 +331,14 @@ int zp_parse_batch_host_multi(zp_ctx* const* ctxs, int nctx, const uint8_t* aren
  * by default a resident server wave of ctx (one wave on one CU, launched on
  * the first call) polls a doorbell there, parses the frame in place and
  * writes the record back: no kernel launch per call.
- * The wave leaves after an idle timeout (5 ms by default) without requests
- * and is relaunched by the next call. While it runs, a device-wide
- * synchronisation (hipDeviceSynchronize, torch.cuda.synchronize, hipFree)
- * waits for it to leave: call zp_parse_one_config first to stop it at once.
- * Frames over 64 KiB take the batch host path. */
+ * The wave leaves after an idle timeout (5 ms by default) without requests,
+ * and after 1 ms resident whatever the traffic; the next call relaunches it
+ * (under steady traffic the host queues the next wave behind the old one).
+ * A device-wide synchronisation (hipDeviceSynchronize,
+ * torch.cuda.synchronize, hipFree) issued meanwhile waits for the running
+ * wave, so at most about 1 ms; zp_parse_one_config stops it at once.
+ * Frames over 64 KiB take the batch host path. Like every zp_ctx call, one
+ * thread at a time per ctx (one context per thread, or a pool). */
 int zp_parse_one(zp_ctx* ctx, const uint8_t* frame, uint64_t len,
                  zp_record* record, zp_ext_offsets ext[2]);
 /* zp_parse_one's mode on ctx: idle_us > 0 = the resident server with that
@@ -343,6 +346,9 @@ int zp_parse_one(zp_ctx* ctx, const uint8_t* frame, uint64_t len,
  * stream wait per call (~18 us). Stops a running server either way.
  * Returns 0, or -1 on a NULL ctx. */
 int zp_parse_one_config(zp_ctx* ctx, uint32_t idle_us);
+/* The calling thread's current HIP device (hipGetDevice), -1 on failure:
+ * the device a facade creates its contexts on. */
+int zp_device_current(void);
 
 /* ------------------------------------------------------------------------- */
 /* Standalone readers and the checksum primitives.                           */

@@ -188,9 +188,10 @@ def test_gpu_columns_vs_oracle(zp, golden, case):
 @pytest.mark.gpu
 def test_parse_with_columns_fresh_arenas(zp):
     """A caller that hands parse_with_columns(mode="auto") a fresh arena per
-    batch: the first four arenas of a shape are timed; once they agree, later
-    arenas of that shape take the agreed path without timing again, and the
-    remembered workloads stay bounded. Results equal the fused path's."""
+    batch: the workload is keyed by shape and stack mix, not by the buffer,
+    so the choice made on the first arenas holds for the later ones (no
+    re-timing per batch); the remembered workloads stay bounded. Results
+    equal the fused path's on every call."""
     import torch
     d = torch.device("cuda:0")
     C = zp.columns
@@ -200,15 +201,62 @@ def test_parse_with_columns_fresh_arenas(zp):
     want_r, _, want_c = C.parse_with_columns(a0, o, l_, names=names, mode="fused")
     keep = []
     t0 = C.auto_timings
-    for k in range(7):
+    for k in range(12):
         a = a0.clone()                                  # a fresh buffer each batch
         keep.append(a)
         r, _, c = C.parse_with_columns(a, o, l_, names=names)
         torch.cuda.synchronize()
         assert torch.equal(r, want_r) and all(torch.equal(c[x], want_c[x]) for x in names), k
-    shape = next(iter(C._agree))
-    seen = C._agree[shape]
-    if len(set(seen[:4])) == 1:                         # the usual case: one path clearly faster
-        assert C.auto_timings - t0 == 4, seen
+    # call 1 (mix unknown) timed once; from call 2 the mix is known: 4 timed
+    # calls, the choice on call 6, none timed after
+    assert C.auto_timings - t0 == 5, C.auto_timings - t0
+    assert C.auto_choice(keep[-1], o.numel(), names) in ("fused", "split")
+    assert C.auto_choice(a0, o.numel(), names) == C.auto_choice(keep[0], o.numel(), names)
     assert len(C._auto) <= C._AUTO_MAX
+    C.reset_auto()
+
+
+@pytest.mark.gpu
+def test_parse_with_columns_reused_arena_changed_traffic(zp, monkeypatch):
+    """One arena buffer reused while its traffic changes from c3 (plain IPv4)
+    to c4 (IPv6 chains behind VLAN tags): the sampled stack mix changes, so
+    the c4 traffic becomes a workload of its own and is timed and decided
+    afresh instead of inheriting c3's choice. No call waits for the device
+    (synchronize is refused while the calls run). Results equal the oracle
+    path's on every call."""
+    import torch
+    d = torch.device("cuda:0")
+    C = zp.columns
+    C.reset_auto()
+    monkeypatch.setattr(C, "_SAMPLE_EVERY", 2)
+    n = 1 << 15
+    a3, o3, l3 = zp.batch.generate("c3", n, first=3, device=d)
+    a4, o4, l4 = zp.batch.generate("c4", n, first=4, device=d)
+    buf = torch.zeros(max(a3.numel(), a4.numel()), dtype=torch.uint8, device=d)
+    names = ["src_addr", "dest_addr", "src_port", "dest_port", "l4_proto"]
+    want = {}
+    for tag, a, o, l_ in (("c3", a3, o3, l3), ("c4", a4, o4, l4)):
+        buf[:a.numel()] = a
+        want[tag] = C.parse_with_columns(buf, o, l_, names=names, mode="fused")
+    torch.cuda.synchronize()
+
+    def refuse(*a, **k):
+        raise AssertionError("parse_with_columns(mode='auto') waited for the device")
+    keys = []
+    for tag, a, o, l_ in (("c3", a3, o3, l3), ("c4", a4, o4, l4)):
+        buf[:a.numel()] = a
+        for k in range(10):
+            with monkeypatch.context() as m:
+                m.setattr(torch.cuda, "synchronize", refuse)
+                m.setattr(torch.cuda.Event, "synchronize", refuse)
+                m.setattr(torch.cuda.Stream, "synchronize", refuse)
+                r, _, c = C.parse_with_columns(buf, o, l_, names=names)
+            torch.cuda.synchronize()                    # the test's own check only
+            wr, _, wc = want[tag]
+            assert torch.equal(r, wr) and all(torch.equal(c[x], wc[x]) for x in names), (tag, k)
+        st = C._shapes[C._shape_key(buf, n, names)]
+        keys.append(st.mix)
+        assert C.auto_choice(buf, n, names) in ("fused", "split"), tag
+    assert keys[0] != keys[1], keys                      # c4 is another workload
+    assert keys[0] == (4, 0, 0), keys                    # c3: all plain IPv4
     C.reset_auto()

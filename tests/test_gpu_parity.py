@@ -934,3 +934,183 @@ def test_parse_one_server_lifecycle(zp, golden):
                 time.sleep(gap)
     finally:
         lib.zp_ctx_destroy(ctx)
+
+
+def _c5_frames(zp, n, seed=5):
+    a, o, l_ = zp.batch.generate_host("c5", n, first=seed)
+    return [a[int(x):int(x) + int(y)].tobytes() for x, y in zip(o, l_)]
+
+
+def test_parse_one_sync_bound_under_traffic(zp):
+    """A thread calls zp_parse_one back to back (one call every ~10-20 us)
+    for 2 s while the main thread times 20 torch.cuda.synchronize() calls:
+    the server leaves after its 1 ms life whatever the traffic (the host
+    queues the next wave behind it), so no synchronisation waits longer than
+    that bound + 1 ms. Control: with a 20 ms life (test hook) the same
+    synchronisations wait for the server, so the test sees it. Every answer
+    equals the oracle's. The GIL switch interval is lowered to 50 us for the
+    test: at Python's 5 ms default, handing the GIL back and forth to the
+    calling thread alone costs the timed thread ~10 ms."""
+    import sys
+    import threading
+    import time
+    R = zp.records
+    frames = _c5_frames(zp, 256)
+    want = [orc.parse_one(f) for f in frames]
+    bufs = [ctypes.create_string_buffer(f, max(len(f), 1)) for f in frames]
+    lib = zp._lib.hip()
+    ctx = lib.zp_ctx_create(0, 1 << 20)
+    assert ctx
+    old_si = sys.getswitchinterval()
+
+    def run(life_us):
+        assert lib.zp__one_test_hooks(ctx, life_us, 0, 0) == 0
+        stop = threading.Event()
+        bad, calls = [], [0]
+
+        def caller():
+            rec = np.zeros(1, R.RECORD_DTYPE)
+            ext = np.zeros((2, 16), np.uint8)
+            k = 0
+            while not stop.is_set():
+                i = k % len(frames)
+                rc = lib.zp_parse_one(ctx, ctypes.addressof(bufs[i]), len(frames[i]),
+                                      rec.ctypes.data, ext.ctypes.data)
+                err, wrec, wext = want[i]
+                if rc != err or rec.tobytes() != orc.pack(wrec, wext).tobytes() \
+                        or ext.tobytes() != wext.view(np.uint8).tobytes():
+                    bad.append((k, i, rc, err))
+                k += 1
+            calls[0] = k
+
+        th = threading.Thread(target=caller)
+        th.start()
+        try:
+            time.sleep(0.1)                               # traffic is steady
+            waits = []
+            t_end = time.perf_counter() + 2.0
+            while len(waits) < 20:
+                t0 = time.perf_counter()
+                torch.cuda.synchronize()
+                waits.append(time.perf_counter() - t0)
+                time.sleep(max(0.0, (t_end - time.perf_counter()) / (21 - len(waits))))
+        finally:
+            stop.set()
+            th.join(30)
+        assert not th.is_alive()
+        print(f"life {life_us} us: {calls[0]} calls; synchronize waits ms: "
+              f"max {1e3 * max(waits):.3f} median {1e3 * sorted(waits)[10]:.3f}")
+        assert not bad, bad[:5]
+        assert calls[0] > 20000                           # the traffic really was steady
+        return waits
+    try:
+        sys.setswitchinterval(5e-5)
+        waits = run(1000)
+        assert max(waits) <= 2.0e-3, waits                # life (1 ms) + 1 ms
+        waits = run(20000)
+        assert sorted(waits)[10] >= 2.0e-3, waits         # control: the sync does wait for it
+    finally:
+        sys.setswitchinterval(old_si)
+        lib.zp_ctx_destroy(ctx)
+
+
+def test_parse_one_giveup_retires_request(zp):
+    """when zp_parse_one gives up waiting (test hook: a 300 us
+    give-up, a 30 ms stall queued in front of the server), the request is
+    retired and the servers are stopped before the call returns, so a late
+    server never answers it from a frame the next call is rewriting; the next
+    calls, on other frames, equal the oracle."""
+    import time
+    R = zp.records
+    frames = _c5_frames(zp, 64, seed=9)
+    want = [orc.parse_one(f) for f in frames]
+    lib = zp._lib.hip()
+    ctx = lib.zp_ctx_create(0, 1 << 20)
+    assert ctx
+    rec = np.zeros(1, R.RECORD_DTYPE)
+    ext = np.zeros((2, 16), np.uint8)
+
+    def call(i):
+        buf = ctypes.create_string_buffer(frames[i], max(len(frames[i]), 1))
+        return lib.zp_parse_one(ctx, ctypes.addressof(buf), len(frames[i]),
+                                rec.ctypes.data, ext.ctypes.data)
+    try:
+        for rep in range(3):
+            assert lib.zp__one_test_hooks(ctx, 0, 300, 30000) == 0
+            t0 = time.perf_counter()
+            assert call(rep) == -2                        # gave up
+            dt = time.perf_counter() - t0
+            assert dt >= 0.025, dt                        # ... after the stall drained
+            assert b"no answer" in lib.zp_last_error()
+            assert lib.zp__one_test_hooks(ctx, 0, 10_000_000, 0) == 0
+            for i in range(8, 64):
+                err, wrec, wext = want[i]
+                assert call(i) == err and rec.tobytes() == orc.pack(wrec, wext).tobytes(), (rep, i)
+                assert ext.tobytes() == wext.view(np.uint8).tobytes(), (rep, i)
+    finally:
+        lib.zp_ctx_destroy(ctx)
+
+
+def test_parse_one_life_rotation(zp):
+    """A 200 us server life: under back-to-back calls the host queues a new
+    wave behind the old one every ~100 us of its clock, each starting from
+    the acknowledgement word; 6,000 answers equal the oracle's (none lost,
+    none answered twice from a rewritten frame)."""
+    R = zp.records
+    frames = _c5_frames(zp, 512, seed=13)
+    want = [orc.parse_one(f) for f in frames]
+    lib = zp._lib.hip()
+    ctx = lib.zp_ctx_create(0, 1 << 20)
+    assert ctx
+    rec = np.zeros(1, R.RECORD_DTYPE)
+    ext = np.zeros((2, 16), np.uint8)
+    rng = np.random.default_rng(4)
+    try:
+        assert lib.zp__one_test_hooks(ctx, 200, 0, 0) == 0
+        for k, i in enumerate(rng.integers(0, len(frames), 6000)):
+            f = frames[i]
+            buf = ctypes.create_string_buffer(f, max(len(f), 1))
+            rc = lib.zp_parse_one(ctx, ctypes.addressof(buf), len(f), rec.ctypes.data,
+                                  ext.ctypes.data)
+            err, wrec, wext = want[i]
+            assert rc == err and rec.tobytes() == orc.pack(wrec, wext).tobytes(), (k, int(i), rc)
+            assert ext.tobytes() == wext.view(np.uint8).tobytes(), (k, int(i))
+    finally:
+        lib.zp_ctx_destroy(ctx)
+
+
+def test_parser_threads_and_current_device(zp, golden):
+    """PacketParser.parse from 8 threads at once: each call leases a context
+    of the current device's pool (no global lock), results equal the
+    single-thread ones; the pool belongs to torch's current device."""
+    import threading
+    P = zp.parser
+    frames = [bytes.fromhex(fx["bytes"]) for fx in golden["fixtures"]]
+    frames += _c5_frames(zp, 200, seed=21)
+
+    def result(f):
+        try:
+            return P.PacketParser.parse(f).debug()
+        except P.ZeroPacketError as e:
+            return repr(e)
+    want = [result(f) for f in frames]
+    assert zp._lib.hip().zp_device_current() == torch.cuda.current_device()
+    got, errs = {}, []
+
+    def worker(t):
+        try:
+            got[t] = [result(f) for f in frames[t::3] + frames]
+        except Exception as e:                            # surfaced below
+            errs.append(repr(e))
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(120)
+    assert not errs, errs
+    for t in range(8):
+        assert got[t] == want[t::3] + want, t
+    pool = P._POOLS[torch.cuda.current_device()]
+    assert pool.device == torch.cuda.current_device()
+    assert 1 <= len(pool.all) <= 8 and all(pool.all)
+    P.quiesce()

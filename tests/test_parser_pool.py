@@ -1,0 +1,127 @@
+"""CPU: PacketParser.parse's context pool (parser.py), over a stand-in for the
+C library (no device calls): contexts are created on the calling thread's
+current device, one per concurrent caller, reused LIFO, frames past ONE_MAX
+take the device's one large context, and quiesce() stops idle contexts only.
+The real library runs the same paths in tests/test_gpu_parity.py
+(test_parser_threads_and_current_device)."""
+import threading
+import time
+
+import numpy as np
+import pytest
+
+
+class FakeLib:
+    """zp_device_current / zp_ctx_create / zp_parse_one / zp_parse_one_config
+    with the C signatures' meaning; zp_parse_one sleeps so calls overlap."""
+
+    def __init__(self):
+        self.device = 0
+        self.created = []          # (handle, device, chunk)
+        self.configured = []
+        self.lock = threading.Lock()
+        self.busy = set()
+        self.overlap = 0
+
+    def zp_device_current(self):
+        return self.device
+
+    def zp_ctx_create(self, device, chunk):
+        with self.lock:
+            h = 1000 + len(self.created)
+            self.created.append((h, device, chunk))
+        return h
+
+    def zp_parse_one(self, ctx, frame, n, rec, ext):
+        with self.lock:
+            assert ctx not in self.busy, "a context served two calls at once"
+            self.busy.add(ctx)
+            self.overlap = max(self.overlap, len(self.busy))
+        time.sleep(0.002)
+        with self.lock:
+            self.busy.discard(ctx)
+        return 0
+
+    def zp_parse_one_config(self, ctx, idle):
+        self.configured.append(ctx)
+        return 0
+
+    def zp_last_error(self):
+        return b""
+
+
+@pytest.fixture
+def fake(zp, monkeypatch):
+    P = zp.parser
+    lib = FakeLib()
+    monkeypatch.setattr(zp._lib, "hip", lambda: lib)
+    monkeypatch.setattr(P, "_POOLS", {})
+    monkeypatch.setattr(P.PacketParser, "from_record",
+                        classmethod(lambda cls, f, r, x: ("ok", len(f))))
+    return lib
+
+
+def test_contexts_follow_current_device(zp, fake):
+    P = zp.parser
+    fake.device = 3
+    assert P.PacketParser.parse(b"\0" * 60) == ("ok", 60)
+    fake.device = 1
+    P.PacketParser.parse(b"\0" * 60)
+    assert [(d, c) for _, d, c in fake.created] == [(3, P.POOL_CHUNK), (1, P.POOL_CHUNK)]
+    assert sorted(P._POOLS) == [1, 3]
+    # reuse: no new context for a sequential caller
+    P.PacketParser.parse(b"\0" * 60)
+    assert len(fake.created) == 2
+
+
+def test_threads_run_concurrently_on_own_contexts(zp, fake):
+    P = zp.parser
+    ths = [threading.Thread(target=lambda: [P.PacketParser.parse(b"\0" * 80) for _ in range(10)])
+           for _ in range(8)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert fake.overlap >= 2                       # no global lock
+    assert len(fake.created) <= 8
+    pool = P._POOLS[0]
+    assert sorted(pool.free) == sorted(pool.all)   # every lease returned
+
+
+def test_pool_bound_waits(zp, fake, monkeypatch):
+    P = zp.parser
+    monkeypatch.setattr(P, "POOL_MAX", 2)
+    ths = [threading.Thread(target=lambda: [P.PacketParser.parse(b"\0" * 80) for _ in range(5)])
+           for _ in range(6)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert len(fake.created) == 2 and fake.overlap == 2
+
+
+def test_long_frames_take_the_large_context(zp, fake):
+    P = zp.parser
+    P.PacketParser.parse(b"\0" * (P.ONE_MAX + 1))
+    P.PacketParser.parse(b"\0" * (P.ONE_MAX + 1))
+    assert [c for _, _, c in fake.created] == [0]          # one 256 MiB-chunk context
+    P.PacketParser.parse(b"\0" * P.ONE_MAX)
+    assert [c for _, _, c in fake.created] == [0, P.POOL_CHUNK]
+
+
+def test_quiesce_touches_idle_contexts_only(zp, fake):
+    P = zp.parser
+    P.PacketParser.parse(b"\0" * 64)
+    pool = P._POOLS[0]
+    held = pool._take()                                    # a call in flight elsewhere
+    P.quiesce()
+    assert held not in fake.configured
+    assert set(fake.configured) == set(pool.free)
+    pool._give(held)
+
+
+def test_device_error_raises(zp, fake):
+    P = zp.parser
+    fake.device = -1
+    with pytest.raises(RuntimeError):
+        P.PacketParser.parse(b"\0" * 64)

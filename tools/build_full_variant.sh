@@ -1,10 +1,14 @@
 #!/bin/bash
-# A whole libzp_hip.so built with extra flags (A/B of host + device code,
-# e.g. tools/parse_one_latency.py --lib tools/variants/<name>):
+# A whole libzp_hip.so built with extra flags from the lab sources (the
+# product plus tools/patches/lab.patch; A/B of host + device code, e.g.
+# tools/parse_one_latency.py --lib tools/variants/<name> with -DZP_ONE_STAMPS):
 #   tools/build_full_variant.sh <name> [flags...]
 cd "$(dirname "$0")/.." || exit 1
 name=$1; shift
-C=zero-packet_amd/csrc
+S=tools/variants/src_$name
+rm -rf "$S" && mkdir -p "$S/zero-packet_amd" && cp -r zero-packet_amd/csrc "$S/zero-packet_amd/" \
+  && cp -r include "$S/" && patch -s -p1 -d "$S" < tools/patches/lab.patch || exit 1
+C=$S/zero-packet_amd/csrc
 O=tools/variants/$name
 mkdir -p "$O"
 objs=()

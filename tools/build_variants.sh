@@ -1,8 +1,16 @@
 #!/bin/bash
 # Builds timing variants of the parse kernel into tools/variants/ (A/B only).
+# The product sources carry no variant or ablation branches: the timing
+# ablations (ZP_ABL_*, ZB_ABL_*), the diagnostic stamps (ZP_STAMPS,
+# ZP_ONE_STAMPS, ZB_STAMPS, ZP_DBG_FBCOUNT) and the rejected layouts
+# (ZP_NO_TAIL) come back from tools/patches/lab.patch, applied to a scratch
+# copy of the sources under tools/variants/src.
 cd "$(dirname "$0")/.." || exit 1
 mkdir -p tools/variants
-C=zero-packet_amd/csrc
+S=tools/variants/src
+rm -rf "$S" && mkdir -p "$S/zero-packet_amd" && cp -r zero-packet_amd/csrc "$S/zero-packet_amd/" \
+  && cp -r include "$S/" && patch -s -p1 -d "$S" < tools/patches/lab.patch || exit 1
+C=$S/zero-packet_amd/csrc
 build() {  # name flags...
   local name=$1; shift
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared "$@" \
@@ -22,9 +30,11 @@ for v in "$@"; do
   case $v in
     nostream)   build nostream -DZP_ABL_STREAM_OFF ;;
     fakewalk)   build fakewalk -DZP_ABL_FAKE_WALK ;;
-    streamonly) build streamonly -DZP_ABL_FAKE_WALK -DZP_ABL_WIN_OFF ;;
-    unroll8)    build unroll8 -DZP_UNROLL=8 ;;
-    unroll2)    build unroll2 -DZP_UNROLL=2 ;;
+    norec)      build norec -DZP_ABL_NOREC ;;
+    norec_fakewalk) build norec_fakewalk -DZP_ABL_NOREC -DZP_ABL_FAKE_WALK ;;
+    stamps)     build stamps -DZP_STAMPS ;;
+    fbcount)    build fbcount -DZP_DBG_FBCOUNT ;;
+    tailfree)   build tailfree -DZP_NO_TAIL=1 -DZP_STARTS=32 ;;
     b-*) name=${v%%:*}; flags=${v#*:}; buildb "${name#b-}" $flags ;;
     c-*) name=${v%%:*}; flags=${v#*:}; buildc "${name#c-}" $flags ;;
     *) name=${v%%:*}; flags=${v#*:}; build "$name" $flags ;;

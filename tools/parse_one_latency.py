@@ -1,14 +1,19 @@
 """zp_parse_one latency (per-frame PacketParser::parse through the GPU):
 builds tools/latency/parse_one_main.cpp against libzp_hip.so and runs it with
-1 and 8 threads (one zp_ctx each) on generated c3 frames.
+1 and 8 threads (one zp_ctx each) on generated c3 frames; then
+PacketParser.parse (the Python facade, one pooled context per concurrent
+call) from 1 and 8 Python threads.
 
-    python tools/parse_one_latency.py [--calls 3000]
+    python tools/parse_one_latency.py [--calls 3000] [--py-threads 1,8]
 """
 import argparse
 import importlib
 import os
+import json
 import subprocess
 import sys
+import threading
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -21,6 +26,7 @@ def main():
     ap.add_argument("--modes", default="5000,0",
                     help="zp_parse_one_config idle_us per run: >0 resident server, 0 launch per call")
     ap.add_argument("--lib", default="", help="directory of another libzp_hip.so build (A/B)")
+    ap.add_argument("--py-threads", default="1,8", help="Python facade thread counts ('' = skip)")
     args = ap.parse_args()
     zp = importlib.import_module("zero-packet_amd")
     a, o, l_ = zp.batch.generate_host("c3", 256)
@@ -37,6 +43,35 @@ def main():
             print(r.stdout.strip() or r.stderr[-2000:], flush=True)
             if r.returncode:
                 sys.exit(r.returncode)
+    frames_b = [a[x:x + y].tobytes() for x, y in zip(o, l_)]
+    for t in [int(x) for x in args.py_threads.split(",") if x]:
+        py_threads(zp, frames_b, t, args.calls)
+
+
+def py_threads(zp, frames, threads, calls):
+    """PacketParser.parse from `threads` Python threads, `calls` each."""
+    P = zp.parser.PacketParser
+    for f in frames[:64]:                                   # warm the pool's servers
+        P.parse(f)
+    lat = [[] for _ in range(threads)]
+
+    def run(t):
+        for k in range(calls):
+            t0 = time.perf_counter()
+            P.parse(frames[(k * 7 + t) % len(frames)])
+            lat[t].append(time.perf_counter() - t0)
+    ths = [threading.Thread(target=run, args=(t,)) for t in range(threads)]
+    t0 = time.perf_counter()
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    dt = time.perf_counter() - t0
+    allv = sorted(x for v in lat for x in v)
+    print(json.dumps({"api": "PacketParser.parse (Python)", "threads": threads,
+                      "calls": len(allv), "p50_us": round(1e6 * allv[len(allv) // 2], 2),
+                      "p99_us": round(1e6 * allv[int(len(allv) * 0.99)], 2),
+                      "calls_per_s": round(len(allv) / dt)}), flush=True)
 
 
 if __name__ == "__main__":

@@ -43,6 +43,8 @@ def hip():
         _sig(lib, "zp_parse_batch_host_multi", i32, [vp, i32, vp, u64, vp, vp, u64, vp, vp])
         _sig(lib, "zp_parse_one", i32, [vp, vp, u64, vp, vp])
         _sig(lib, "zp_parse_one_config", i32, [vp, u32])
+        _sig(lib, "zp_device_current", i32, [])
+        _sig(lib, "zp__one_test_hooks", i32, [vp, u32, u64, u32])   # test hook
         _sig(lib, "zp_col_width", i32, [i32])
         _sig(lib, "zp_build_err_str", ctypes.c_char_p, [i32])
         _sig(lib, "zp_build_batch_device", i32, [vp, vp, vp, u64, vp, vp, vp, vp, vp])

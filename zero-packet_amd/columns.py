@@ -75,31 +75,64 @@ def extract(arena, offs, lens, records, names=None, out=None, stream=None, check
     return {k: out[k] for k in names}
 
 
-# Path choice of parse_with_columns(mode="auto") per workload key: the fused
+# Path choice of parse_with_columns(mode="auto") per workload: the fused
 # kernel (one pass) wins on most traffic, but plain IPv4 frames with wide
 # column requests run faster as parse + extract (round 4/5: c3 with all 29
-# columns +2-5 % fused; c4/c5/c6 -11 to -23 %). The library
-# times both paths on the first call of a workload and keeps the faster one.
-_AUTO_REPS = 2             # timed back-to-back runs per path (after one warm-up run)
-_AUTO_MAX = 256            # workload keys remembered (least recently used dropped)
-_AUTO_AGREE = 4            # arenas of one (device, columns, size octave) whose timings agree
-_auto = collections.OrderedDict()
-_agree = {}                # (device, columns, octave) -> the choices timed so far
-auto_timings = 0           # first calls that timed both paths (diagnostics, tests)
+# columns +2-5 % fused; c4/c5/c6 -11 to -23 %).
+#
+# A workload is its shape (device, column set, batch-size octave) and the
+# traffic's stack mix: shares of plain IPv4, of IPv6 extension chains and of
+# IP-in-IP among 256 records sampled from a call of that shape (copied back
+# asynchronously and read on a later call once its event has completed, every
+# _SAMPLE_EVERY calls per shape, so a reused arena whose traffic changes is
+# re-classified). An undecided workload alternates the two paths, one per
+# call, each between two timing events; once both have _AUTO_REPS completed
+# timings, the faster is kept. Nothing here waits for the device: events are
+# only queried, and every call runs exactly one path.
+_AUTO_REPS = 2             # completed timings per path before a choice
+_AUTO_MAX = 256            # workloads remembered (least recently used dropped)
+_SAMPLE = 256              # records sampled per mix reading
+_SAMPLE_EVERY = 16         # calls per shape between two mix readings
+_auto = collections.OrderedDict()   # workload key -> "fused" | "split"
+_timing = {}               # undecided workload key -> {"fused": [...], "split": [...], "pending": [...]}
+_shapes = {}               # shape -> _ShapeState
+auto_timings = 0           # timed runs started (diagnostics, tests)
 
 
-def _auto_key(arena, n, names):
-    # the arena buffer too: traffic of another shape arrives in another buffer
-    # (c3 and c4 batches of one size want different paths, tools/cols_policy.py)
-    return (arena.device.index, arena.data_ptr(), tuple(sorted(names)), max(n, 1).bit_length())
+class _ShapeState:
+    def __init__(self):
+        self.mix = None            # current stack-mix class (None: not read yet)
+        self.calls = 0
+        self.pending = None        # (pinned sample, event) of a mix reading in flight
+        self.host = None           # pinned sample buffer
+        self.idx = None            # device sample indices (for self.n)
+        self.n = -1
+
+
+def _shape_key(arena, n, names):
+    return (arena.device.index, tuple(sorted(names)), max(n, 1).bit_length())
+
+
+def _mix_class(sample):
+    """Stack-mix class of sampled records (uint8 [k, 8]): quarters of the
+    plain-IPv4, extension-chain and IP-in-IP shares among accepted frames."""
+    from .records import F_EXT, F_INNER_EXT, F_IP_IN_IP, F_IPV4
+    w = sample.numpy().view(np.uint32).reshape(-1, 2)
+    flags, offs = w[:, 0], w[:, 1]
+    ok = (flags >> 26) == 0
+    k = max(int(ok.sum()), 1)
+    v4 = ok & ((flags & F_IPV4) != 0) & ((flags & F_IP_IN_IP) == 0)
+    chain = ok & (((flags & (F_EXT | F_INNER_EXT)) != 0) | ((offs >> 31) != 0))
+    inner = ok & ((flags & F_IP_IN_IP) != 0)
+    q = lambda m: int(round(4 * int(m.sum()) / k))
+    return (q(v4), q(chain), q(inner))
 
 
 def reset_auto():
-    """Forgets every choice of parse_with_columns(mode="auto") (the traffic in
-    a reused arena changed shape): the next call of each workload times both
-    paths again."""
+    """Forgets every choice and mix reading of parse_with_columns(mode="auto")."""
     _auto.clear()
-    _agree.clear()
+    _timing.clear()
+    _shapes.clear()
 
 
 def _remember(key, choice):
@@ -110,9 +143,42 @@ def _remember(key, choice):
 
 
 def auto_choice(arena, n, names):
-    """The path parse_with_columns(mode="auto") uses for this workload key
-    (None before its first call)."""
-    return _auto.get(_auto_key(arena, n, names))
+    """The path parse_with_columns(mode="auto") uses for this shape and the
+    traffic mix read last (None while undecided)."""
+    sk = _shape_key(arena, n, names)
+    st = _shapes.get(sk)
+    return _auto.get(sk + ((st.mix if st else None),))
+
+
+def _read_mix(st):
+    if st.pending is not None and st.pending[1].query():
+        st.mix = _mix_class(st.pending[0])
+        st.pending = None
+
+
+def _sample_mix(st, records, n, ts):
+    """Queues a copy of _SAMPLE records (evenly spaced) to pinned memory."""
+    k = min(_SAMPLE, n)
+    if st.n != n:
+        st.idx = torch.linspace(0, n - 1, k, device=records.device).round().long()
+        st.host = torch.empty((k, 8), dtype=torch.uint8, pin_memory=True)
+        st.n = n
+    with torch.cuda.stream(ts):
+        st.host.copy_(records.index_select(0, st.idx), non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(ts)
+    st.pending = (st.host, ev)
+
+
+def _collect(t):
+    """Moves the completed timings of an undecided workload into its lists."""
+    left = []
+    for path, a, b in t["pending"]:
+        if b.query():
+            t[path].append(a.elapsed_time(b))
+        else:
+            left.append((path, a, b))
+    t["pending"] = left
 
 
 def parse_with_columns(arena, offs, lens, names=None, records=None, ext=None, out=None,
@@ -122,10 +188,13 @@ def parse_with_columns(arena, offs, lens, names=None, records=None, ext=None, ou
     mode: "fused" = zp_parse_batch_columns_device (one pass over the frames);
     "split" = zp_parse_batch_device then zp_extract_columns_device on the same
     stream; "auto" (default) = the faster of the two for this workload (device,
-    arena buffer, column set, batch-size octave; reset_auto() forgets the
-    choices): its first call runs each path once, then
-    twice back to back between HIP events on the launch stream, keeps the
-    faster, and synchronises; later calls of the workload run that path."""
+    column set, batch-size octave and the stack mix of the traffic, read from
+    sampled records; reset_auto() forgets the choices). Every call runs one
+    path and returns without waiting for the device: while a workload is
+    undecided its calls alternate the paths between timing events, and the
+    first call after both paths have two completed timings fixes the choice.
+    Under stream capture "auto" runs the known choice (or the fused path)
+    with no events and no sampling."""
     for t in (arena, offs, lens):
         if not t.is_cuda:
             raise RuntimeError("columns.parse_with_columns needs device tensors (no CPU fallback)")
@@ -161,46 +230,52 @@ def parse_with_columns(arena, offs, lens, names=None, records=None, ext=None, ou
                                                  lens.data_ptr(), records.data_ptr(), n, ptrs, s),
                    "zp_extract_columns_device")
     paths = {"fused": fused, "split": split}
-    if mode != "auto":
-        paths[mode]()
+    if mode != "auto" or n == 0:
+        paths[mode if mode != "auto" else "fused"]()
         return records, ext, {k: out[k] for k in names}
-    key = _auto_key(arena, n, names)
+    if torch.cuda.is_current_stream_capturing():
+        # under graph capture: no timing events, no mix readings
+        sk = _shape_key(arena, n, names)
+        st = _shapes.get(sk)
+        paths[_auto.get(sk + ((st.mix if st else None),)) or "fused"]()
+        return records, ext, {k: out[k] for k in names}
+    ts = torch.cuda.ExternalStream(stream, device=d) if stream is not None else \
+        torch.cuda.current_stream(d)
+    sk = _shape_key(arena, n, names)
+    st = _shapes.get(sk)
+    if st is None:
+        st = _shapes[sk] = _ShapeState()
+        while len(_shapes) > _AUTO_MAX:
+            del _shapes[next(iter(_shapes))]
+    _read_mix(st)
+    key = sk + (st.mix,)
     choice = _auto.get(key)
-    shape = (key[0],) + key[2:]
-    if choice is None and n:
-        # A caller that hands over a fresh arena per batch: once the first
-        # _AUTO_AGREE arenas of this shape agreed, new ones take that path
-        # without timing it again.
-        seen = _agree.get(shape, [])
-        if len(seen) >= _AUTO_AGREE and len(set(seen)) == 1:
-            choice = seen[0]
-            _remember(key, choice)
+    if choice is not None:
+        _auto.move_to_end(key)
+        paths[choice]()
     else:
-        if choice is not None:
-            _auto.move_to_end(key)
-    if choice is None and n:
-        # First call of this workload: each path once to warm up, then twice
-        # back to back between two events (as a stream of calls runs), and
-        # the faster is kept. Every run writes the same outputs.
-        ts = torch.cuda.ExternalStream(stream, device=d) if stream is not None else \
-            torch.cuda.current_stream(d)
-        ms = {}
-        for k in ("fused", "split"):
-            paths[k]()
+        t = _timing.setdefault(key, {"fused": [], "split": [], "pending": []})
+        _collect(t)
+        if len(t["fused"]) >= _AUTO_REPS and len(t["split"]) >= _AUTO_REPS:
+            choice = min(("fused", "split"), key=lambda p: min(t[p]))
+            _remember(key, choice)
+            del _timing[key]
+            paths[choice]()
+        else:
+            # time the path with fewer timings (counting those in flight)
+            nf = len(t["fused"]) + sum(1 for p, _, _ in t["pending"] if p == "fused")
+            ns = len(t["split"]) + sum(1 for p, _, _ in t["pending"] if p == "split")
+            path = "fused" if nf <= ns else "split"
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record(ts)
-            for _ in range(_AUTO_REPS):
-                paths[k]()
+            paths[path]()
             b.record(ts)
-            b.synchronize()
-            ms[k] = a.elapsed_time(b)
-        global auto_timings
-        auto_timings += 1
-        choice = min(ms, key=ms.get)
-        _remember(key, choice)
-        _agree.setdefault(shape, []).append(choice)
-        if len(_agree[shape]) > 64:
-            del _agree[shape][:-64]
-        return records, ext, {k: out[k] for k in names}
-    paths[choice or "fused"]()
+            t["pending"].append((path, a, b))
+            global auto_timings
+            auto_timings += 1
+            if len(_timing) > _AUTO_MAX:
+                del _timing[next(iter(_timing))]
+    if st.pending is None and (st.mix is None or st.calls % _SAMPLE_EVERY == 0):
+        _sample_mix(st, records, n, ts)
+    st.calls += 1
     return records, ext, {k: out[k] for k in names}

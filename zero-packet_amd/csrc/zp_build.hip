@@ -30,19 +30,11 @@
 extern "C" char* zp__errbuf(void);
 
 #define ZB_WAVES 4
-#ifndef ZB_CAP
 #define ZB_CAP 1536            // frame bytes staged in LDS per frame
-#endif
 #define ZB_LDS (ZB_CAP + 32)   // + the frame's offset in its first 16-B chunk
-#ifndef ZB_OPS
 #define ZB_OPS 4               // ops of a chain prefetched to LDS (longer chains read the rest)
-#endif
-#ifndef ZB_WPE
 #define ZB_WPE 4               // waves per SIMD: 128 VGPRs (5 spilled at 96: 13 % slower on
-#endif                         // payload-copy chains), 29 KB LDS per workgroup
-#ifndef ZB_G
 #define ZB_G 16                // lanes per frame: a wave builds 64 / ZB_G frames side by side
-#endif
 #define ZB_F (64 / ZB_G)       // frames per wave
 #define ZB_PENDING 0xFFu       // results[i].err: left by the lane path for the lane-group pass
 
@@ -307,9 +299,6 @@ struct NoWin {
 // Executes one chain (all checks of the reference, in its order). Returns
 // the zp_build_err; *hl_out = header_len after the last Ok op, *hw_out = an
 // upper bound of the bytes written ([0, hw)).
-#ifndef ZB_OP_NEXT
-#define ZB_OP_NEXT 0
-#endif
 template <int MODE, typename P, typename OPS, typename WC>
 __device__ __forceinline__ int run_chain(BView<P>& v, const uint8_t ZB_LDSP* stage, uint32_t shift,
                          const OPS& ops, uint32_t nops, const WC& wc,
@@ -325,17 +314,8 @@ __device__ __forceinline__ int run_chain(BView<P>& v, const uint8_t ZB_LDSP* sta
     st = BS_RAW;
     uint32_t hl = 0, hw = 0;
     const uint32_t n = v.n;
-#if ZB_OP_NEXT
-    zp_build_op nxt{};
-    if (nops) nxt = ops.get(0);                      // an empty chain loads nothing
-#endif
     for (uint32_t k = 0; k < nops; ++k) {
-#if ZB_OP_NEXT
-        const zp_build_op o = nxt;                   // op k+1's load overlaps op k
-        if (k + 1 < nops) nxt = ops.get(k + 1);
-#else
         const zp_build_op o = ops.get(k);
-#endif
         const int prev = st;
         st = bnext(st, o.kind);
         const bool has = o.data_len != ZP_BUILD_NO_DATA;
@@ -541,9 +521,7 @@ __device__ __forceinline__ int run_chain(BView<P>& v, const uint8_t ZB_LDSP* sta
 }
 
 #define ZB_KATTR __launch_bounds__(64 * ZB_WAVES) __attribute__((amdgpu_waves_per_eu(ZB_WPE)))
-#ifndef ZB_SCAN
 #define ZB_SCAN 16             // 64-frame spans scanned per wave of the pending pass
-#endif
 
 // Frame i on a group of ZB_G lanes (slot = the group's LDS slot).
 __device__ __forceinline__ void build_frame(uint64_t i, int slot, int lane,
@@ -691,12 +669,7 @@ struct OpGlobal {
 // ZB_OP_PREFETCH: the heads of a chain's first ZB_OPH ops are loaded before
 // the stream (their latency hides behind it), chain_extent reads them from
 // registers after it; later ops are loaded then.
-#ifndef ZB_OP_PREFETCH
-#define ZB_OP_PREFETCH 1
-#endif
-#ifndef ZB_OPH
 #define ZB_OPH 4
-#endif
 struct OpHeads {
     OpGlobal og;
     uint2 h[ZB_OPH];
@@ -716,9 +689,6 @@ struct OpHeads {
         return k < ZB_OPH ? (head(k).x & 0xFFu) : og.kind(k);
     }
 };
-#ifndef ZB_OP_KINDS
-#define ZB_OP_KINDS 1          // run_chain's typestate pass reads the prefetched kinds
-#endif
 
 __device__ __forceinline__ uint32_t sad4(uint4 q) {
     return sad16(q.w, sad16(q.z, sad16(q.y, sad16(q.x, 0u))));
@@ -839,46 +809,7 @@ __device__ __forceinline__ uint32_t chain_extent(const Ops& ops, uint32_t nops, 
     return top;
 }
 
-#ifndef ZB_FAST_WPE
 #define ZB_FAST_WPE 3          // at least 3 waves per SIMD (168 VGPRs): the LDS allows 3
-#endif
-#ifndef ZB_LANE_PAY
-#define ZB_LANE_PAY 1          // payload copies past the window on the lane path
-#endif
-#ifndef ZB_SKIP_PAY
-#define ZB_SKIP_PAY 1          // payload frames stream their window only (ZB_LANE_PAY, ZB_OP_PREFETCH)
-#endif
-#if ZB_SKIP_PAY && !(ZB_LANE_PAY && ZB_OP_PREFETCH)
-#error "ZB_SKIP_PAY needs ZB_LANE_PAY and ZB_OP_PREFETCH"
-#endif
-#ifndef ZB_MARK
-#define ZB_MARK 1              // V of the bytes a copy replaces from the stream (no first pass)
-#endif
-#if ZB_MARK && defined(ZB_NO_SECTOR_WB)
-#error "ZB_MARK needs the T4 stream"
-#endif
-#ifndef ZB_PAY_HDR
-#define ZB_PAY_HDR 1           // the wave copy moves the whole payload (the chain copies none of it)
-#endif
-#ifndef ZB_WIDE_EDGES
-#define ZB_WIDE_EDGES 1        // partial 16-B chunks by dword/short/byte stores (0: byte loop)
-#endif
-
-// Diagnostic build only (-DZB_STAMPS, tools/build_bench.py --stamps): per-wave
-// s_memrealtime stamps at the phase boundaries of zp_build_fast_kernel.
-#ifdef ZB_STAMPS
-__device__ unsigned long long* zb_stamp_buf;
-#define ZB_STAMP(i)                                                               \
-    do {                                                                          \
-        const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();           \
-        if (zb_stamp_buf && threadIdx.x == 0) zb_stamp_buf[blockIdx.x * 8 + (i)] = t_; \
-    } while (0)
-extern "C" int zb_stamps_set(void* p) {
-    return hipMemcpyToSymbol(HIP_SYMBOL(zb_stamp_buf), &p, sizeof p) == hipSuccess ? 0 : -1;
-}
-#else
-#define ZB_STAMP(i) do {} while (0)
-#endif
 
 // Wave-cooperative segments: lane j owns cnt_j chunks; the wave walks the
 // concatenation of all lanes' chunks in items of 64 (lane l of item i takes
@@ -889,15 +820,10 @@ extern "C" int zb_stamps_set(void* p) {
 // ZB_COOP_U items' loads are in flight per wave. Returns, per lane, the
 // wrapping sum of its own chunks' contributions (running-sum differences:
 // no segmented reduction). Every lane must be active (DPP scans, bpermute).
-#ifndef ZB_COOP_U
 #define ZB_COOP_U 8            // round 4, with ZB_SKIP_PAY and ZB_COPY_X4: 8 vs 4 P = 1000 -1.1 %, P = 200 -0.2 %; round 3, without ZB_PIPE_SEARCH 1: 2.04 / 3.52 ms, 2: 1.95 / 3.16, 4: 1.99 / 3.26, 8: 2.11 / 3.52 (P = 200 / 1000); with it 2: 1.85 / 2.80, 4: 1.82 / 2.71, 8: 1.82 / 2.70
-#endif
 // ZB_PIPE_SEARCH: the owner search of the next ZB_COOP_U items (dependent
 // ds_bpermute round trips) is issued while this round's loads are in flight,
 // not after its stores.
-#ifndef ZB_PIPE_SEARCH
-#define ZB_PIPE_SEARCH 1
-#endif
 template <class D, class L, class U>
 __device__ __forceinline__ uint32_t wave_segments(uint32_t cnt, int lane, L&& load, U&& use) {
     const uint32_t incl = wave_scan(cnt), pre = incl - cnt;
@@ -916,23 +842,16 @@ __device__ __forceinline__ uint32_t wave_segments(uint32_t cnt, int lane, L&& lo
         }
     };
     uint32_t jj[ZB_COOP_U], kk[ZB_COOP_U];
-#if ZB_PIPE_SEARCH
     if (T) search(0, jj, kk);
-#endif
     for (uint32_t base = 0; base < T; base += 64 * ZB_COOP_U) {
         D d[ZB_COOP_U];
-#if !ZB_PIPE_SEARCH
-        search(base, jj, kk);
-#endif
 #pragma unroll
         for (int u = 0; u < ZB_COOP_U; ++u)
             d[u] = load(jj[u], kk[u], base + 64u * u + (uint32_t)lane < T);
         uint32_t ju[ZB_COOP_U], ku[ZB_COOP_U];
 #pragma unroll
         for (int u = 0; u < ZB_COOP_U; ++u) ju[u] = jj[u], ku[u] = kk[u];
-#if ZB_PIPE_SEARCH
         if (base + 64 * ZB_COOP_U < T) search(base + 64 * ZB_COOP_U, jj, kk);
-#endif
 #pragma unroll
         for (int u = 0; u < ZB_COOP_U; ++u) {
             const uint32_t b = base + 64u * u;
@@ -1046,7 +965,6 @@ __device__ __forceinline__ uint32_t coop_payload(bool go, uintptr_t W, uintptr_t
             const uint32_t v = range_sum(c.q, c.l, c.h);
             return c.neg ? 0u - v : v;
         });
-    ZB_STAMP(3);
     // pass 2: the copy, chunks of [D0a, D1); chunk k holds bytes [lo, m)
     const uintptr_t D0a = D0 & ~(uintptr_t)15;
     const uint32_t o0 = go ? (uint32_t)(D0 - D0a) : 0u;
@@ -1100,13 +1018,7 @@ __device__ __forceinline__ uint32_t coop_payload(bool go, uintptr_t W, uintptr_t
             if (full) {
                 *(ZP_GLOBAL zp_u32x4*)c.X = zp_u32x4{q.x, q.y, q.z, q.w};
             } else if (!(defer0 && lo)) {         // (a first chunk with header bytes: the caller)
-#if ZB_WIDE_EDGES
                 store_bytes(c.X, q, lo, m);
-#else
-                const uint32_t w[4] = {q.x, q.y, q.z, q.w};
-                for (uint32_t b = lo; b < m; ++b)
-                    *(ZP_GLOBAL uint8_t*)(c.X + b) = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
-#endif
             }
             return range_sum(q, lo, m);
         });
@@ -1119,21 +1031,14 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
                      const zp_build_op* __restrict__ ops, const uint32_t* __restrict__ op_start,
                      const uint8_t* __restrict__ data, zp_build_result* __restrict__ results) {
     __shared__ WaveLds lds;
-#ifndef ZB_NO_SECTOR_WB
     // the 3 chunks before each frame's last one (the previous frame's bytes
     // in a frame's first 64-B sector)
     __shared__ uint4 t4[64 * ZP_T4N];
     __shared__ uint32_t cmid[64];                      // running sum at each frame's mark
     constexpr bool T4 = true;
-#else
-    uint4* t4 = nullptr;
-    uint32_t* cmid = nullptr;
-    constexpr bool T4 = false;
-#endif
     const int lane = threadIdx.x & 63;
     const uint64_t t = blockIdx.x;
     if (t * 64 >= n) return;
-    ZB_STAMP(0);
     const uintptr_t fallback = (uintptr_t)&zp_safe_chunk;
     uint4* win = &lds.win[0];
     uint4* tail = &lds.win[ZP_WIN_CH * 64];
@@ -1145,11 +1050,8 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
     const uint32_t pf0 = op_start[ipc], pf1 = op_start[ipc + 1];
     load_desc(arena, offs, lens, n, t, lane, len, ga);
     TileState s;
-#if ZB_OP_PREFETCH && ZB_LANE_PAY
     OpHeads oh{OpGlobal{ops + (ip < n ? pf0 : 0u)}};
     oh.load(ip < n && pf1 >= pf0 ? pf1 - pf0 : 0u);
-#endif
-#if ZB_SKIP_PAY
     // A frame whose final payload copy replaces at least as many bytes past
     // the window as follow the copy streams its window only (wo): the bytes
     // the copy replaces are never read, the ones after it are read by the
@@ -1167,15 +1069,10 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
         if (chain_extent(oh, pf1 - pf0, &pa, &pl) <= wl0 && pl && pa + pl > wl0) {
             const uint32_t pe = pa + pl;
             wo = pe <= len && pe - wl0 >= len - pe;
-            if (ZB_MARK && !wo && pe < len) mark = pe;
+            if (!wo && pe < len) mark = pe;
         }
     }
     tile_setup(s, t, len, ga, n, lane, lds, wo, mark);
-#else
-    const bool wo = false;
-    const uint32_t mark = ~0u;
-    tile_setup(s, t, len, ga, n, lane, lds);
-#endif
     uint4 va[ZP_G];
     uint32_t ka[ZP_G];
     issue_group<ZP_G, T4>(0, s.nitems, s.cur, s.R, lane, fallback, va, ka);
@@ -1185,7 +1082,6 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
         consume_group<ZP_G, T4>(i0, s.nitems, lane, va, ka, win, tail, lds.cend, s.run, t4, cmid);
     }
     wave_lds_fence();                                  // windows written by other lanes
-    ZB_STAMP(1);
     // Every lane stays to the neighbour exchange after the chains; frames
     // that are not built here are marked pending for the lane-group pass.
     const uint64_t i = t * 64 + lane;
@@ -1198,33 +1094,22 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
         o0 = pf0;
         const uint32_t o1 = pf1;
         nops = o1 >= o0 ? o1 - o0 : 0u;
-#if ZB_LANE_PAY
         // A final payload copy may reach past the window: the headers must
         // fit it; the copy's bytes past it go straight to HBM after the chain.
         if (o1 >= o0 && len >= 64 && !s.giant) {
-#if ZB_OP_PREFETCH
             fast = chain_extent(oh, nops, &pay_at, &pay_len, &pay_ovl) <= s.wlen;
-#else
-            fast = chain_extent(OpGlobal{ops + o0}, nops, &pay_at, &pay_len) <= s.wlen;
-#endif
             pay = fast && pay_len && pay_at + pay_len > s.wlen;
         }
-#else
-        fast = o1 >= o0 && len >= 64 && !s.giant && chain_extent(OpGlobal{ops + o0}, nops) <= s.wlen;
-#endif
         if (!fast) {
             zp_build_result r;
             r.header_len = 0; r.err = (uint8_t)ZB_PENDING; r.ops_done = 0; r.reserved = 0;
             results[i] = r;
         }
     }
-#if !(ZB_OP_PREFETCH && ZB_OP_KINDS && ZB_LANE_PAY)
-    const OpGlobal og{ops + o0};
-#endif
     // ph: the wave copy moves the whole payload (ZB_PAY_HDR), unless it
     // overwrites the L4 header's own fields (a TCP data offset below 5: the
     // chain keeps the reference's write order then)
-    const bool ph = ZB_PAY_HDR && pay && !pay_ovl;
+    const bool ph = pay && !pay_ovl;
     const uint32_t rank = s.rank & 63u;
     const uint32_t nch = (len + s.shift + 15) >> 4;
     WinCsum wc;
@@ -1257,21 +1142,13 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
         }
         wc.region = region;
         BView<uint8_t ZB_LDSP*> v{region + s.shift, len, true};
-#if ZB_LANE_PAY
         // The whole wave copies the payload after the chain (coop_payload;
         // without ZB_PAY_HDR the chain writes its window part), and the L4
         // checksum is refolded with that copy's V change below.
         if (pay) v.lim = ph ? pay_at : s.wlen;
-#endif
-#if ZB_OP_PREFETCH && ZB_OP_KINDS && ZB_LANE_PAY
         err = run_chain<ZB_M_WIN>(v, (const uint8_t ZB_LDSP*)nullptr, s.shift, oh, nops, wc,
-#else
-        err = run_chain<ZB_M_WIN>(v, (const uint8_t ZB_LDSP*)nullptr, s.shift, og, nops, wc,
-#endif
                                   data, lane, &hl, &done, &hw, &doff, &lkind);
     }
-    ZB_STAMP(2);
-#if ZB_LANE_PAY
     {
         // A copy that does not fit the frame failed in the chain before any
         // byte was written (err != 0): nothing to copy then. The headers fit
@@ -1297,19 +1174,17 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
         }
         // a marked frame: V of the original bytes [W, D1) from the running
         // sum at the copy's end minus the frame's start and window chunks
-        const bool known = ZB_MARK && go && mark != ~0u;
+        const bool known = go && mark != ~0u;
         const uint32_t vrep = known ? cmid[rank] - (rank ? lds.cend[rank - 1] : 0u) - Vw : 0u;
         const uint32_t delta = coop_payload(go, s.ga + s.wlen, s.ga + (ph ? pay_at : s.wlen),
-                                            s.ga + pe, s.ga + len, src, cB, lane, wo, ZB_PAY_HDR,
+                                            s.ga + pe, s.ga + len, src, cB, lane, wo, true,
                                             known, vrep);
-        ZB_STAMP(4);
         if (go) {                                      // refold the L4 checksum
             const uint32_t k4 = lkind;                  // the chain's last op (go: all ran)
             const uint32_t at = k4 == ZP_B_TCP ? 16u : k4 == ZP_B_UDP ? 6u : 2u;
             const uint16_t c = fold_v(wc.cs_V + delta - vw, wc.cs_acc, !((s.ga + wc.cs_l4) & 1));
             region[s.shift + wc.cs_l4 + at] = (uint8_t)(c >> 8);
             region[s.shift + wc.cs_l4 + at + 1] = (uint8_t)c;
-#if ZB_PAY_HDR
             // The chunk holding the payload's first byte, when it also holds
             // header bytes: those from the region (the checksum refolded),
             // the payload's from the blob again (a line the copy has just
@@ -1338,10 +1213,8 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
                 }
                 *(ZP_GLOBAL zp_u32x4*)((s.ga & ~(uintptr_t)15) + 16u * c0) = zp_u32x4{m[0], m[1], m[2], m[3]};
             }
-#endif
         }
     }
-#endif
     // Write-back of frame bytes [0, hw) from the region: whole 16-B chunks as
     // one store, edge chunks byte by byte (never a byte another lane writes).
     // A store that covers part of a 64-B HBM sector costs ~2.4 x a whole one
@@ -1353,33 +1226,22 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
     // frame ends exactly here and its lane writes nothing there.
     const uintptr_t a0 = s.ga & ~(uintptr_t)15;
     const uint32_t sh = s.shift;
-#if ZB_LANE_PAY
     const bool pay_go = pay && err == 0;               // the chain copied the payload
-#endif
     const uint32_t hwc = hw < s.wlen ? hw : s.wlen;               // hw <= extent <= wlen
     uint32_t end = fast ? sh + hwc : sh;                          // window coordinates
-#ifndef ZB_NO_SECTOR_WB
     if (fast) {
         const uint32_t se = (uint32_t)(((s.ga + hwc + 63) & ~(uintptr_t)63) - a0);
         const uint32_t fe = sh + len;
         const uint32_t e1 = se < fe ? se : fe;                    // never past the frame
         if (hwc && e1 <= sh + s.wlen) end = e1;                   // bytes in the window
     }
-#endif
-#if ZB_LANE_PAY && ZB_PAY_HDR
     // the payload's chunks (from the one holding its first byte) are the copy's
     if (pay_go && ph) {
         const uint32_t pc = (sh + pay_at) & ~15u;
         end = end < pc ? end : pc;
     }
-#endif
-#ifndef ZB_NO_SECTOR_WB
     // the previous lane's frame and where its writes end (all lanes active)
-#if ZB_LANE_PAY
     const uintptr_t wend = pay_go ? s.ga + pay_at + pay_len : a0 + end;
-#else
-    const uintptr_t wend = a0 + end;
-#endif
     const uint32_t pl = lane ? (uint32_t)lane - 1u : 0u;
     const uintptr_t pA = ((uintptr_t)bperm((uint32_t)(s.ga >> 32), pl) << 32) |
                          bperm((uint32_t)s.ga, pl);
@@ -1401,25 +1263,16 @@ zp_build_fast_kernel(uint8_t* __restrict__ arena, const uint64_t* __restrict__ o
             *(ZP_GLOBAL zp_u32x4*)X = zp_u32x4{q.x, q.y, q.z, q.w};
         }
     }
-#else
-    const bool pre = false;
-#endif
     for (uint32_t c = 0; c < ((end + 15) >> 4); ++c) {
         const uint32_t lo = 16 * c, hi = lo + 16;
         if ((lo >= sh || (pre && c == 0)) && hi <= end) {
             const uint4 q = ld_region(region, lo);
             *(ZP_GLOBAL zp_u32x4*)(a0 + lo) = zp_u32x4{q.x, q.y, q.z, q.w};
         } else {
-#if ZB_WIDE_EDGES
             const uint32_t bs = lo < sh ? sh : lo, be = hi < end ? hi : end;
             if (bs < be) store_bytes(a0 + lo, ld_region(region, lo), bs - lo, be - lo);
-#else
-            for (uint32_t b = lo < sh ? sh : lo; b < (hi < end ? hi : end); ++b)
-                *(ZP_GLOBAL uint8_t*)(a0 + b) = region[b];
-#endif
         }
     }
-    ZB_STAMP(5);
     if (!fast) return;
     zp_build_result r;
     r.header_len = hl;
@@ -1455,10 +1308,8 @@ extern "C" int zp_build_batch_device(uint8_t* arena, const uint64_t* offs, const
     }
     hipLaunchKernelGGL(zp_build_fast_kernel, dim3((unsigned)fast_blocks), dim3(64), 0, st, arena,
                        offs, lens, n, ops, op_start, data, res);
-#ifndef ZB_ABL_NO_SECOND   // timing ablation only (tools/build_variants.sh)
     hipLaunchKernelGGL(zp_build_kernel, dim3((unsigned)blocks), dim3(64 * ZB_WAVES), 0, st, arena,
                        offs, lens, n, ops, op_start, data, res);
-#endif
     if (!results) (void)hipFreeAsync(res, st);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {

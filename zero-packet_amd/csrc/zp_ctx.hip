@@ -15,6 +15,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <immintrin.h>
 #include <pthread.h>
 #include <time.h>
 
@@ -57,11 +58,15 @@ struct zp_ctx {
     bool one_failed;              // the mapped block could not be allocated: batch path
     // ... and its resident server wave (zp_one_server_kernel, zp_parse.hip)
     uint32_t one_idle_us;         // server idle timeout; 0: one batch launch per call
+    uint32_t one_life_us;         // server residency bound (ONE_LIFE_US_DEFAULT)
     uint64_t one_clock_khz;       // the device's constant clock (s_memrealtime)
-    uint32_t one_seq;             // last request the server finished
+    uint32_t one_seq;             // last request answered (or retired by a stop)
     hipStream_t srv;              // the server's stream
     bool srv_live;                // a server was launched and may still run
     int64_t srv_seen_ns;          // host clock when the server last showed activity
+    int64_t srv_born_ns;          // host clock when the newest server was launched
+    int64_t one_giveup_ns;        // no answer for this long: the request fails (-2)
+    uint32_t one_stall_us;        // test hook: a stall kernel before each server launch
 };
 
 // zp_parse_one's block: the frame at ONE_FRAME, the doorbell and the batch
@@ -73,19 +78,25 @@ struct zp_ctx {
 #define ONE_LENS 16      // uint32_t (launch mode)
 #define ONE_REC 64       // zp_record (8 B)
 #define ONE_ACK 72       // uint32_t: seq of the last finished request (server mode), written
-                         // with the record by one 16-B store
+                         // with the record by one 16-B store ...
+#define ONE_TAG 76       // ... and the tag rec.x ^ rec.y ^ seq ^ ONE_TAG_KEY
 #define ONE_EXT 96       // zp_ext_offsets[2]
 #define ONE_FRAME 128
 #define ONE_MAX (64u << 10)
 #define ONE_STOP 0xFFFFFFFFu          // doorbell length: the server leaves
 #define ONE_IDLE_US_DEFAULT 5000u     // server idle timeout
+#define ONE_LIFE_US_DEFAULT 1000u     // a server leaves after this long resident, busy or not
 #define ONE_MARGIN_NS 500000          // host/device clock slack when judging the server alive
+#define ONE_LIFE_MARGIN_NS 100000     // ... and before its life ends (the host relaunches it)
+#define ONE_GIVEUP_NS 10000000000ll   // 10 s without an answer: the request fails
+#define ONE_TAG_KEY 0x9E3779B9u       // ZP_ONE_TAG (zp_parse.hip)
 
 static_assert(ONE_FRAME + ONE_MAX + 64 == 128u + (64u << 10) + 64u,
               "the server's buffer range (ZP_SYS_BYTES, zp_stream.h) is the mapped block");
 
-extern "C" int zp__one_server_launch(uint8_t* blk_d, uint32_t seq, uint64_t idle_ticks,
+extern "C" int zp__one_server_launch(uint8_t* blk_d, uint64_t idle_ticks, uint64_t life_ticks,
                                      void* stream);
+extern "C" int zp__one_stall_launch(uint64_t ticks, void* stream);
 
 static int64_t mono_ns() {
     timespec t;
@@ -117,15 +128,19 @@ static hipError_t grow(T** p, uint64_t* cap, uint64_t need) {
         }                                                                          \
     } while (0)
 
-// Stops the context's zp_parse_one server (if one may run) and waits for it.
+// Stops the context's zp_parse_one servers (the running one and any queued
+// behind it) and waits for them. Every one of them leaves without answering
+// a request: a server starts from the acknowledgement word, and the stop
+// doorbell is newer. The stop's seq then becomes the acknowledgement, so the
+// next launch starts from it.
 static void one_server_stop(zp_ctx* c) {
     if (!c->srv_live) return;
-    const uint64_t bell = ((uint64_t)(c->one_seq + 1u) << 32) | ONE_STOP;
-    __atomic_store_n((uint64_t*)(c->one_h + ONE_BELL), bell, __ATOMIC_RELEASE);
+    const uint32_t stop = c->one_seq + 1u;
+    __atomic_store_n((uint64_t*)(c->one_h + ONE_BELL), ((uint64_t)stop << 32) | ONE_STOP,
+                     __ATOMIC_RELEASE);
     (void)hipStreamSynchronize(c->srv);
-    // a server that had already left never saw the stop: the doorbell keeps
-    // seq + 1, so the next launch starts from there
-    c->one_seq += 1u;
+    c->one_seq = stop;
+    __atomic_store_n((uint32_t*)(c->one_h + ONE_ACK), stop, __ATOMIC_RELEASE);
     c->srv_live = false;
 }
 
@@ -160,6 +175,8 @@ extern "C" zp_ctx* zp_ctx_create(int device, uint64_t chunk_bytes) {
     c->device = device;
     c->chunk_bytes = chunk_bytes;
     c->one_idle_us = ONE_IDLE_US_DEFAULT;
+    c->one_life_us = ONE_LIFE_US_DEFAULT;
+    c->one_giveup_ns = ONE_GIVEUP_NS;
     c->chunk_pkts = chunk_bytes / 64 + 1;
     (void)hipGetDevice(&prev);
     TRY(hipSetDevice(device));
@@ -338,49 +355,87 @@ static bool one_block(zp_ctx* c) {
     return c->one_h != NULL;
 }
 
+// Launches a server behind whatever runs on the server stream (a server
+// about to reach its life waits for nothing more than that).
+static int one_server_launch(zp_ctx* c, int64_t now) {
+    const uint64_t idle = (uint64_t)c->one_idle_us * c->one_clock_khz / 1000u;
+    const uint64_t life = (uint64_t)c->one_life_us * c->one_clock_khz / 1000u;
+    if (c->one_stall_us) {
+        const int rc = zp__one_stall_launch((uint64_t)c->one_stall_us * c->one_clock_khz / 1000u,
+                                            c->srv);
+        if (rc) return rc;
+    }
+    const int rc = zp__one_server_launch(c->one_d, idle, life, c->srv);
+    if (rc) return rc;
+    c->srv_live = true;
+    c->srv_seen_ns = now;
+    c->srv_born_ns = now;
+    return 0;
+}
+
+// True when the server surely still runs: it answered less than its idle
+// timeout ago and it was launched less than its life ago (host clock; the
+// device counts both from later instants, so the estimate is conservative).
+static bool one_server_sure(const zp_ctx* c, int64_t now) {
+    return c->srv_live && now - c->srv_seen_ns < (int64_t)c->one_idle_us * 1000 - ONE_MARGIN_NS &&
+           now - c->srv_born_ns < (int64_t)c->one_life_us * 1000 - ONE_LIFE_MARGIN_NS;
+}
+
 // One request through the resident server: doorbell, then spin on the
-// acknowledgement. The server is (re)launched when it is not running; the
-// host's clock says when it surely still runs (less than its idle timeout
-// since it last acknowledged), otherwise the stream says whether it left.
-static int one_via_server(zp_ctx* c, uint32_t len) {
-    int64_t now = mono_ns();
-    const int64_t idle_ns = (int64_t)c->one_idle_us * 1000;
-    if (c->srv_live && now - c->srv_seen_ns >= idle_ns - ONE_MARGIN_NS) {
-        const hipError_t q = hipStreamQuery(c->srv);
-        if (q == hipSuccess) c->srv_live = false;          // it left
-        else if (q != hipErrorNotReady) {
-            snprintf(g_ctx_error, ERRBUF_LEN, "zp_parse_one server: %s", hipGetErrorString(q));
-            return -2;
+// acknowledgement. When the server may have left (or is about to, at its
+// life), a new one is queued behind it on its stream first; it starts from
+// the acknowledgement word, so nothing is answered twice. The answer is the
+// 16-B {record, ack, tag} read as one load; an ack whose tag does not match
+// the record read with it is waited out (a host-link write seen in pieces).
+// On giving up, the request is retired and the servers stopped before the
+// block is written again (a late server must not answer it from a frame
+// being rewritten).
+static int one_via_server(zp_ctx* c, uint32_t len, zp_record* out, bool sure, int64_t now) {
+    if (!sure) {                                             // the caller set the device
+        // Launch when no server runs, or queue the next one behind the
+        // running one when its life is nearly over; a running one whose idle
+        // timeout may have passed answers, or, if it just left, the check
+        // below relaunches (rare: the window is the host link's latency).
+        bool launch = !c->srv_live;
+        if (!launch) {
+            const hipError_t q = hipStreamQuery(c->srv);
+            if (q == hipSuccess) launch = true;
+            else if (q != hipErrorNotReady) {
+                snprintf(g_ctx_error, ERRBUF_LEN, "zp_parse_one server: %s", hipGetErrorString(q));
+                c->srv_live = false;
+                return -2;
+            } else {
+                launch = now - c->srv_born_ns >= (int64_t)c->one_life_us * 1000 - ONE_LIFE_MARGIN_NS;
+            }
+        }
+        if (launch) {
+            const int rc = one_server_launch(c, now);
+            if (rc) return rc;
         }
     }
-    const uint64_t ticks = (uint64_t)c->one_idle_us * c->one_clock_khz / 1000u;
-    if (!c->srv_live) {
-        const int rc = zp__one_server_launch(c->one_d, c->one_seq, ticks, c->srv);
-        if (rc) return rc;
-        c->srv_live = true;
-        c->srv_seen_ns = now;
-    }
     const uint32_t seq = c->one_seq + 1u;
-    volatile uint32_t* ack = (volatile uint32_t*)(c->one_h + ONE_ACK);
+    const volatile __m128i* ans = (const volatile __m128i*)(c->one_h + ONE_REC);
     __atomic_store_n((uint64_t*)(c->one_h + ONE_BELL), ((uint64_t)seq << 32) | len,
                      __ATOMIC_RELEASE);
     const int64_t t0 = now;
     int64_t next_check = t0 + 200000;                        // 200 us
+    uint32_t w[4];
     for (uint32_t spin = 1;; ++spin) {
-        if (__atomic_load_n(ack, __ATOMIC_ACQUIRE) == seq) break;
-        __builtin_ia32_pause();
+        const __m128i v = _mm_load_si128((const __m128i*)ans);
+        _mm_storeu_si128((__m128i*)w, v);
+        if (w[2] == seq && w[3] == (w[0] ^ w[1] ^ seq ^ ONE_TAG_KEY)) break;
+        _mm_pause();
         if ((spin & 1023u) == 0) {
             now = mono_ns();
             if (now < next_check) continue;
-            // The server may have left just before the doorbell (its idle
-            // timeout): then its stream is done and the request still open.
+            // The servers may all have left before the doorbell (their
+            // timeouts): then the stream is done and the request still open.
             const hipError_t q = hipStreamQuery(c->srv);
             if (q == hipSuccess) {
-                if (__atomic_load_n(ack, __ATOMIC_ACQUIRE) == seq) break;
                 int prev = 0;
                 (void)hipGetDevice(&prev);
                 (void)hipSetDevice(c->device);
-                const int rc = zp__one_server_launch(c->one_d, c->one_seq, ticks, c->srv);
+                const int rc = one_server_launch(c, now);
                 (void)hipSetDevice(prev);
                 if (rc) return rc;
             } else if (q != hipErrorNotReady) {
@@ -388,7 +443,13 @@ static int one_via_server(zp_ctx* c, uint32_t len) {
                 c->srv_live = false;
                 return -2;
             }
-            if (now - t0 > 10000000000ll) {                  // 10 s: give up
+            if (now - t0 > c->one_giveup_ns) {
+                int prev = 0;
+                (void)hipGetDevice(&prev);
+                (void)hipSetDevice(c->device);
+                c->one_seq = seq;                           // retired: never answered later
+                one_server_stop(c);
+                (void)hipSetDevice(prev);
                 snprintf(g_ctx_error, ERRBUF_LEN, "zp_parse_one: no answer from the server");
                 return -2;
             }
@@ -397,6 +458,7 @@ static int one_via_server(zp_ctx* c, uint32_t len) {
     }
     c->one_seq = seq;
     c->srv_seen_ns = mono_ns();
+    memcpy(out, w, sizeof(zp_record));
     return 0;
 }
 
@@ -411,12 +473,12 @@ extern "C" int zp_parse_one(zp_ctx* c, const uint8_t* frame, uint64_t len,
     if (!c || !record || len > 0xFFFFFFFFull || (!frame && len)) return -1;
     int rc;
     uint8_t* h = c->one_h;
-    if (h && len <= ONE_MAX && c->one_idle_us && c->srv_live &&
-        mono_ns() - c->srv_seen_ns < (int64_t)c->one_idle_us * 1000 - ONE_MARGIN_NS) {
-        // The fast path: the server surely runs (it answered less than its
-        // idle timeout ago), so no HIP call at all: copy, doorbell, spin.
+    const int64_t now = mono_ns();
+    if (h && len <= ONE_MAX && c->one_idle_us && one_server_sure(c, now)) {
+        // The fast path: the server surely runs, so no HIP call at all:
+        // copy, doorbell, spin.
         if (len) memcpy(h + ONE_FRAME, frame, len);
-        rc = one_via_server(c, (uint32_t)len);
+        rc = one_via_server(c, (uint32_t)len, record, true, now);
     } else {
         int prev = 0;
         (void)hipGetDevice(&prev);
@@ -433,7 +495,7 @@ extern "C" int zp_parse_one(zp_ctx* c, const uint8_t* frame, uint64_t len,
         h = c->one_h;
         if (len) memcpy(h + ONE_FRAME, frame, len);
         if (c->one_idle_us) {
-            rc = one_via_server(c, (uint32_t)len);
+            rc = one_via_server(c, (uint32_t)len, record, false, now);
         } else {
             const uint64_t at = ONE_FRAME;
             const uint32_t l = (uint32_t)len;
@@ -450,11 +512,11 @@ extern "C" int zp_parse_one(zp_ctx* c, const uint8_t* frame, uint64_t len,
                     rc = -2;
                 }
             }
+            if (!rc) memcpy(record, h + ONE_REC, sizeof(zp_record));
         }
         (void)hipSetDevice(prev);
     }
     if (rc) return rc;
-    memcpy(record, h + ONE_REC, sizeof(zp_record));
     if (ext) {
         // entries are defined only where the record flags them (zero_packet.h)
         const zp_ext_offsets* x = (const zp_ext_offsets*)(h + ONE_EXT);
@@ -466,13 +528,6 @@ extern "C" int zp_parse_one(zp_ctx* c, const uint8_t* frame, uint64_t len,
     return (int)zp_rec_err(*record);
 }
 
-#ifdef ZP_ONE_STAMPS   // diagnostic build only: the server's last stamps
-extern "C" void zp__one_stamps(zp_ctx* c, uint64_t* out) {
-    memcpy(out, c->one_h + 32, 32);
-    memcpy(out + 4, c->one_h + 24, 8);
-    memcpy(out + 6, c->one_h + ONE_FRAME + ONE_MAX, 8 * 8);  // phase stamps (OSTAMP 0-7)
-}
-#endif
 
 // zp_parse_one's mode: idle_us = 0 launches the batch kernel per call;
 // otherwise a resident server wave answers and leaves after idle_us without
@@ -486,6 +541,30 @@ extern "C" int zp_parse_one_config(zp_ctx* c, uint32_t idle_us) {
     one_server_stop(c);
     c->one_idle_us = idle_us;
     (void)hipSetDevice(prev);
+    return 0;
+}
+
+extern "C" int zp_device_current(void) {
+    int d = -1;
+    const hipError_t e = hipGetDevice(&d);
+    if (e != hipSuccess) {
+        snprintf(g_ctx_error, ERRBUF_LEN, "hipGetDevice: %s", hipGetErrorString(e));
+        return -1;
+    }
+    return d;
+}
+
+// Test hook (tests/test_gpu_parity.py, not in zero_packet.h): the server's
+// life and the give-up time in us (0: keep), and a stall of stall_us queued
+// in front of every server launch (0: none). Stops a running server.
+extern "C" int zp__one_test_hooks(zp_ctx* c, uint32_t life_us, uint64_t giveup_us,
+                                  uint32_t stall_us) {
+    if (!c) return -1;
+    const int rc = zp_parse_one_config(c, c->one_idle_us);
+    if (rc) return rc;
+    if (life_us) c->one_life_us = life_us;
+    if (giveup_us) c->one_giveup_ns = (int64_t)giveup_us * 1000;
+    c->one_stall_us = stall_us;
     return 0;
 }
 

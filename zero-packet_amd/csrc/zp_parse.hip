@@ -41,53 +41,19 @@
 // at most 96 VGPRs, so 18 waves fit a CU instead of 16. Measured per
 // placement in one process against the 128-B window at 108 VGPRs: c5 -6 %,
 // c3 and c4 within +-1 %.
-#ifndef ZP_WIN
 #define ZP_WIN 112
-#endif
-#ifndef ZP_WPE
 #define ZP_WPE 5
-#endif
 #include "zp_stream.h"
 
-#ifndef ZP_WAVES
 #define ZP_WAVES 1           // waves per workgroup (independent waves; 1 = finest LDS granularity)
-#endif
-#ifndef ZP_EXT_DENSE
 #define ZP_EXT_DENSE 32      // chains per wave from which all 64 ext entries are written
-#endif
-#ifndef ZP_K
 #define ZP_K 1               // consecutive tiles per wave
-#endif
-#ifndef ZP_FAST_V4
-#define ZP_FAST_V4 1         // straight-line path for Ethernet/IPv4(IHL 5)/TCP|UDP|ICMPv4 (0: off)
-#endif
-#ifndef ZP_TINY
-#define ZP_TINY 1            // register path for tiles of 64-B Ethernet/IPv4/L4 frames (0: off)
-#endif
-#ifndef ZP_SMALL_G
 #define ZP_SMALL_G 4         // tiles of at most this many stream items take one small group (0: off)
-#endif
-#ifndef ZP_TAIL_G
 #define ZP_TAIL_G 4          // a tile's last <= this many items as one small group (0: off)
-#endif
-#ifndef ZP_EARLY_REC
-#define ZP_EARLY_REC 1       // the record stored before the verdict (0: after it)
-#endif
-#ifndef ZP_TAIL_G2
-#define ZP_TAIL_G2 1         // ... and the last <= 2 as a pair (c5 -0.5 %, c6 -0.6 %)
-#endif
-// Timing-only ablations and diagnostics (tools/build_variants.sh,
-// tools/alloc_probe.py --no-check); never set in the product:
-//   ZP_ABL_FAKE_WALK  replace the walk by "pending L4 at offset 42"
-//   ZP_ABL_STREAM_OFF skip the stream loads
-//   ZP_ABL_NOSCAN     no per-item wave scan (zp_stream.h)
-//   ZP_ABL_EXTRA=n    n extra dependent VALU per stream item (zp_stream.h)
-//   ZP_ABL_NO_IPSUM / ZP_ABL_NO_PSEUDO / ZP_ABL_NO_L4HDR  skip one header sum
-//   ZP_ABL_NO_L1      fast_ip without its second IP level
-//   ZP_ABL_NOREC      no record stores
-//   ZP_ABL_REC4       4-B record stores at 4 * i (wrong contents, timing only)
-//   ZP_STAMPS         per-wave phase timestamps (tools/stamps.py)
-//   ZP_DBG_FBCOUNT    count past-window chunk loads (tools/fbcount.py)
+// Rejected variants, timing ablations and diagnostic stamps live in
+// tools/patches/lab.patch, applied to a scratch copy by
+// tools/build_variants.sh (tools/kbench.py --variants); this file is the
+// product kernel only.
 
 static __thread char g_last_error[256];
 
@@ -119,57 +85,21 @@ __device__ __forceinline__ bool icmpv6_type_ok(uint32_t t) {
     return t >= 128 && t <= 153;
 }
 
-// Diagnostic build only (-DZP_STAMPS): per-wave s_memrealtime stamps at the
-// phase boundaries, written to their own buffer (never read by the kernel).
-#ifdef ZP_STAMPS
-#define ZP_NSTAMP 8
-__device__ unsigned long long* zp_stamp_buf;
-#define STAMP(i)                                                               \
-    do {                                                                       \
-        unsigned long long t_ = __builtin_amdgcn_s_memrealtime();              \
-        if (zp_stamp_buf && lane == 0) zp_stamp_buf[wave_id * ZP_NSTAMP + (i)] = t_; \
-    } while (0)
-extern "C" int zp_stamps_set(void* p) {
-    return hipMemcpyToSymbol(HIP_SYMBOL(zp_stamp_buf), &p, sizeof p) == hipSuccess ? 0 : -1;
-}
-#else
-#define STAMP(i) do {} while (0)
-#endif
-// Diagnostic build only (-DZP_ONE_STAMPS): the resident zp_parse_one server's
-// phase stamps, written into the spare 64 B at the end of its host block
-// (128 + 64 KiB + 8 i, past the largest frame; zp__one_stamps).
-#ifdef ZP_ONE_STAMPS
-#define OSTAMP(i)                                                              \
-    do {                                                                       \
-        if (SYS && sysbase && lane == 0)                                       \
-            __hip_atomic_store((uint64_t*)(sysbase + 65664 + 8 * (i)),         \
-                               __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, \
-                               __HIP_MEMORY_SCOPE_SYSTEM);                     \
-    } while (0)
-#else
-#define OSTAMP(i) do {} while (0)
-#endif
-
 // --------------------------------------------------------------------------
 // Frame view: LDS window (16-B cells, chunk c of frame f at win[c][f ^ c]:
 // conflict-free for the cooperative ds_write_b128 of phase A and for each
 // lane's ds_read_b128 of its own frame) + global fallback past the window.
 // --------------------------------------------------------------------------
-// ZP_REGION: after the stream each lane copies its frame's window cells out
+// After the stream each lane copies its frame's window cells out
 // of the swizzled [chunk][rank] layout into a private contiguous LDS region of
 // ZP_RSTRIDE dwords (an odd count: the lanes' reads of one offset fall in 64
 // different banks), so a field read is one ds_read_b32 at region + (y >> 2)
 // instead of a swizzled-cell address (5 VALU) with 4-way bank conflicts.
-#ifndef ZP_REGION
-#define ZP_REGION 1
-#endif
 #define ZP_RSTRIDE (ZP_WIN / 4 + 1)
 struct FrameView {
     const uint4* win;        // this wave's window, [ZP_WIN_CH][64]
-#if ZP_REGION
-    const uint32_t* reg;     // ZP_REGION: this lane's window, ZP_WIN / 4 dwords from A & ~15
+    const uint32_t* reg;     // this lane's window, ZP_WIN / 4 dwords from A & ~15
     bool region;             // reg is set (a constant per kernel: the one-frame server reads the cells)
-#endif
     const uint8_t* g;        // frame in global memory
     uint32_t lane;
     uint32_t shift;          // frame address & 15 (window starts 16-aligned)
@@ -178,76 +108,28 @@ struct FrameView {
     uint4 xc;                // past the window: one cached 16-B chunk ...
     uint32_t xi;             // ... and its index from A & ~15 (~0: none)
     uintptr_t sysbase;       // != 0: the frame lies in the host block at sysbase (system-scope loads)
-#ifdef ZP_FB2
-    uint4 xc2;               // A/B: and the chunk after it
-#endif
-#ifdef ZP_DBG_FBCOUNT
-    uint64_t seen = 0;       // diagnostics: past-window chunks (< 64) loaded so far
-#endif
 };
 
 __device__ __forceinline__ uint4 win_chunk(const FrameView& f, uint32_t c) {
-#if ZP_REGION
     if (f.region) return make_uint4(f.reg[4 * c], f.reg[4 * c + 1], f.reg[4 * c + 2], f.reg[4 * c + 3]);
     return f.win[c * 64 + (f.lane ^ c)];
-#else
-    return f.win[c * 64 + (f.lane ^ c)];
-#endif
 }
 __device__ __forceinline__ uint32_t win_dw(const FrameView& f, uint32_t d) {
-#if ZP_REGION
     if (f.region) return f.reg[d];
     const uint32_t c = d >> 2;
     return ((const uint32_t*)&f.win[c * 64 + (f.lane ^ c)])[d & 3];
-#else
-    const uint32_t c = d >> 2;
-    return ((const uint32_t*)&f.win[c * 64 + (f.lane ^ c)])[d & 3];
-#endif
 }
 
 // Chunk c (from A & ~15) past the window: one 16-B load per distinct chunk
 // (deep IPv6 extension chains and IP-in-IP read a few bytes each from the
 // same chunks).
-#ifdef ZP_DBG_FBCOUNT   // diagnostic build only (tools/fbcount.py): fallback chunk loads
-__device__ unsigned long long zp_fb_count, zp_fb_repeat;
-extern "C" unsigned long long zp_dbg_fb_count(void) {
-    unsigned long long v = 0, z = 0;
-    (void)hipMemcpyFromSymbol(&v, HIP_SYMBOL(zp_fb_count), sizeof v);
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(zp_fb_count), &z, sizeof z);
-    return v;
-}
-// ... of which loads of a chunk this frame's walk had loaded before
-extern "C" unsigned long long zp_dbg_fb_repeat(void) {
-    unsigned long long v = 0, z = 0;
-    (void)hipMemcpyFromSymbol(&v, HIP_SYMBOL(zp_fb_repeat), sizeof v);
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(zp_fb_repeat), &z, sizeof z);
-    return v;
-}
-#endif
 __device__ __forceinline__ uint4 fb_chunk(FrameView& f, uint32_t c) {
-#ifdef ZP_FB2
-    // A/B: a miss loads chunks c and c + 1 together (the walk moves forward)
-    if (c != f.xi && c != f.xi + 1) {
-        const uintptr_t b = ((uintptr_t)f.g & ~(uintptr_t)15) + 16u * c;
-        const uint32_t last = (f.len + f.shift - 1) >> 4;    // never past the frame's last chunk
-        f.xc = ldg16(b);
-        f.xc2 = c + 1 <= last ? ldg16(b + 16) : f.xc;
-        f.xi = c;
-    }
-    return c == f.xi ? f.xc : f.xc2;
-#else
     if (c != f.xi) {
-#ifdef ZP_DBG_FBCOUNT
-        atomicAdd(&zp_fb_count, 1ull);
-        if (c < 64 && ((f.seen >> c) & 1ull)) atomicAdd(&zp_fb_repeat, 1ull);
-        if (c < 64) f.seen |= 1ull << c;
-#endif
         const uintptr_t a = ((uintptr_t)f.g & ~(uintptr_t)15) + 16u * c;
         f.xc = f.sysbase ? ld_sys16(f.sysbase, a) : ldg16(a);
         f.xi = c;
     }
     return f.xc;
-#endif
 }
 
 __device__ __forceinline__ uint32_t dw_of(uint4 v, uint32_t d) {
@@ -356,31 +238,10 @@ __device__ __forceinline__ uint32_t sum_to(FrameView& f, uint32_t x) {
 // addresses, V = E + 256*O and B = E + O, so O = (V - B) / 255 exactly; the
 // words start at an even address iff A + lo is even.
 __device__ __forceinline__ uint32_t sumW_exact(FrameView& f, uint32_t lo, uint32_t hi) {
-#ifndef ZP_SUMW_BYTES
     uint32_t V, B;
     sum_vb<true>(f, lo, hi, V, B);
     const uint32_t O = (V - B) / 255u, E = B - O;
     return (((uintptr_t)f.g + lo) & 1) ? 256u * O + E : 256u * E + O;
-#else   // A/B reference: dword-wise from the window, bytewise past it
-    uint32_t E = 0, O = 0;
-    for (uint32_t x = lo; x < hi; x += 4) {
-        uint32_t v;
-        const int n = (int)(hi - x) < 4 ? (int)(hi - x) : 4;
-        if (x + 3 < f.wlen) {
-            const uint32_t y = x + f.shift, d = y >> 2;
-            const uint32_t a = win_dw(f, d);
-            const uint32_t b = (y & 3) ? win_dw(f, d + 1) : 0u;
-            v = __builtin_amdgcn_alignbyte(b, a, y & 3);
-        } else {
-            v = 0;
-            for (int k = 0; k < n; ++k) v |= rd8(f, x + k) << (8 * k);
-        }
-        v &= byte_mask(0, 0, n);
-        E += (v & 0xFFu) + ((v >> 16) & 0xFFu);
-        O += ((v >> 8) & 0xFFu) + (v >> 24);
-    }
-    return 256u * E + O;
-#endif
 }
 
 // Pseudo-header word sum modulo 65535. For frames of <= 64 KiB the verdict
@@ -554,14 +415,10 @@ __device__ __forceinline__ void walk_frame(FrameView& f, Walk& w) {
                     if (ihl < 20) { err = ZP_ERR_IPV4_IHL_TOO_SHORT; goto done; }
                     if (sl < ihl) { err = ZP_ERR_IPV4_HDR_TOO_LONG; goto done; }
                     if (rd16(f, pos + 2) != sl) { err = ZP_ERR_IPV4_TOTAL_LENGTH; goto done; }
-#ifdef ZP_ABL_NO_IPSUM
-                    const uint32_t hv = 65535u;                        // timing ablation only
-#else
                     // ipv4.rs:262-264; a 20-B header inside the window (the
                     // common case) straight-line (c5 -4 %)
                     const uint32_t hv = (ihl == 20 && pos + 20 <= f.wlen)
                                             ? wsum4<5>(f, pos + f.shift) : sumV(f, pos, pos + ihl);
-#endif
                     if (!nz_mod65535_zero(hv)) { err = ZP_ERR_IPV4_CHECKSUM; goto done; }
                     proto = rd8(f, pos + 9);
                     pp = pos + ihl;
@@ -634,9 +491,6 @@ __device__ __forceinline__ void walk_frame(FrameView& f, Walk& w) {
                 // none for ICMPv4), parser.rs:341-361 (IPv6, final next header).
                 // One pseudo-header sum for both IP versions (the address range differs,
                 // the code does not: no divergent duplicate).
-#ifdef ZP_ABL_NO_PSEUDO
-                const uint32_t ps = 0;                                // timing ablation only
-#else
                 const uint32_t plo = v4 ? pos + 12 : pos + 8, phi = v4 ? pos + 20 : pos + 40;
                 uint32_t ps;
                 if (len > ZP_GIANT) ps = sumW_exact(f, plo, phi);
@@ -645,7 +499,6 @@ __device__ __forceinline__ void walk_frame(FrameView& f, Walk& w) {
                     ps = (((uintptr_t)f.g + plo) & 1) ? V : V * 256u;   // (c5 -1 %)
                 }
                 else ps = sumW_mod(f, plo, phi);
-#endif
                 w.acc = (v4 && proto == 1) ? 0u : ps + proto + (len - pp);
                 r.l4_off = pp;
                 w.pending = 1;
@@ -758,12 +611,7 @@ __device__ __forceinline__ bool fast_v4(const FrameView& f, const Probe& pr, Wal
 // every frame of >= 82 bytes has them there; a shorter one fails that
 // level's `pos + 20 <= len` check whatever the bytes past it hold.
 // --------------------------------------------------------------------------
-#ifndef ZP_FAST_IP
-#define ZP_FAST_IP 1
-#endif
-#if ZP_FAST_IP
 static_assert(ZP_WIN - 15 >= 82, "fast_ip reads frame bytes up to 81 from the window");
-#endif
 struct IpLevel { uint32_t proto, next; bool ok; };
 // One IP level at `pos` (parser.rs:188-212 with a 20-B header / 222-230
 // without extension headers), both versions computed, `v4` selecting.
@@ -802,12 +650,7 @@ __device__ __forceinline__ bool fast_ip(FrameView& f, const Probe& pr, Walk& w) 
     const IpLevel L0 = ip_level(f, hl, v4o);                            // parse_ipv4 / parse_ipv6
     const bool enc = L0.proto == 4 || L0.proto == 41;                   // parser.rs:134-135
     const bool v4i = L0.proto == 4;
-#ifdef ZP_ABL_NO_L1   // timing ablation only: no second IP level (wrong records)
-    IpLevel L1 = L0;
-    L1.next = L0.next + 20u;
-#else
     const IpLevel L1 = ip_level(f, L0.next, v4i);
-#endif
     ok = ok && L0.ok && (!enc || (L1.ok && L1.proto != 4 && L1.proto != 41));
     const uint32_t proto = enc ? L1.proto : L0.proto;
     const uint32_t pp = enc ? L1.next : L0.next;
@@ -840,11 +683,7 @@ __device__ __forceinline__ bool fast_ip(FrameView& f, const Probe& pr, Walk& w) 
     w.l4 = pp;
     w.v6 = v4 ? 0 : 1;
     w.acc = 0;
-#ifdef ZP_ABL_NO_PSEUDO   // timing ablation only
-    if (false) {
-#else
     if (ok && l4 && !(v4 && ic4)) {
-#endif
         // pseudo-header of the innermost IP (parser.rs:316-333, 341-361)
         const uint32_t plo = v4 ? ipl + 12 : ipl + 8, phi = v4 ? ipl + 20 : ipl + 40;
         uint32_t ps;
@@ -915,23 +754,13 @@ __device__ __forceinline__ bool tiny_tile(uint64_t tile, uint32_t len, uintptr_t
     if (live) {
         // Ethernet II (code 0), IPv4, the L4 reader at 34
         const uint32_t flags = ZP_F_ETHERNET | ZP_F_IPV4 | (tcp ? ZP_F_TCP : udp ? ZP_F_UDP : ZP_F_ICMPV4);
-#ifdef ZP_ABL_REC4
-        __builtin_nontemporal_store(flags ^ 34u, (uint32_t*)records + tile * 64 + lane);
-#else
         __builtin_nontemporal_store(zp_u32x2{flags, 34u}, (zp_u32x2*)(records + tile * 64 + lane));
-#endif
     }
     return true;
 }
 
 __device__ __forceinline__ void store_ext(zp_ext_offsets* base, uint64_t i, uint4 q) {
-#ifdef ZP_ABL_EXT8
-    // Timing probe only (wrong contents): the store pattern of an 8-B entry
-    // array, entry i at byte 8 * i of the same buffer.
-    __builtin_nontemporal_store(zp_u32x2{q.x ^ q.z, q.y ^ q.w}, (zp_u32x2*)base + i);
-#else
     __builtin_nontemporal_store(zp_u32x4{q.x, q.y, q.z, q.w}, (zp_u32x4*)(base + i));
-#endif
 }
 
 // Header walk + checksum verdict + record store of a streamed tile; with COLS
@@ -943,14 +772,11 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
                                             const ColPtrs& cols, uintptr_t sysbase = 0,
                                             zp_u32x2* sys_rec = nullptr) {
     constexpr bool TAILS = sizeof(lds.win) > sizeof(uint4) * ZP_WIN_CH * 64;   // last-chunk cells
-    static_assert(TAILS || (ZP_REGION && !SYS), "the tail-free layout needs the region path");
+    static_assert(TAILS || !SYS, "the tail-free layout needs the region path");
     uint4* tail = TAILS ? &lds.win[0] + ZP_WIN_CH * 64 : nullptr;
     const uint8_t* g = (const uint8_t*)s.ga;
     // the frame's stream sum (before the regions overlay the running sums)
     const uint32_t fsum = lds.cend[s.rank & 63u] - ((s.rank & 63u) ? lds.cend[(s.rank & 63u) - 1u] : 0u);
-#ifdef ZP_STAMPS
-    const uint64_t wave_id = s.tile;
-#endif
     FrameView fv;
     fv.win = &lds.win[0];
     fv.g = g;
@@ -961,7 +787,6 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
     fv.xc = make_uint4(0, 0, 0, 0);
     fv.xi = ~0u;
     fv.sysbase = SYS ? sysbase : 0;
-#if ZP_REGION
     // the frame's cells and last chunk to registers, then its window to the
     // lane's private region (it overlays the cells and part of the tails);
     // the one-frame tile of the zp_parse_one server (SYS) reads the cells
@@ -977,22 +802,7 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
         uint4 cell[ZP_WIN_CH];
 #pragma unroll
         for (uint32_t c = 0; c < ZP_WIN_CH; ++c) cell[c] = lds.win[c * 64 + ((rk ^ c) & 63u)];
-        if (TAILS) {
-            mytail = tail[rk];
-        } else {
-            // The bytes past the frame's end in its last chunk: the next
-            // rank's first window cell when that is the same 16-B chunk
-            // (frames back to back), else the chunk from memory (the tile's
-            // last frame, gaps, other orders).
-            const uint32_t nr = (rk + 1u) & 63u;
-            const uint4 ncell = lds.win[nr];                   // chunk 0 of rank rk + 1
-            const uintptr_t nA = ((((uintptr_t)bperm(s.R.org_hi, nr)) << 32) | bperm(s.R.org_lo, nr)) +
-                                 16ull * bperm(s.R.pfx, nr);
-            const uintptr_t lastc = (s.ga + s.len - 1u) & ~(uintptr_t)15;
-            const bool nxt = rk + 1u < s.cur.nz && nA == lastc;
-            const bool need = s.live && s.len >= 64 && !s.giant && ((s.len + s.shift) & 15u) != 0u;
-            mytail = nxt ? ncell : (need ? ldg16(lastc) : make_uint4(0, 0, 0, 0));
-        }
+        mytail = tail[rk];
         wave_lds_fence();
         uint32_t* reg = (uint32_t*)&lds.win[0] + (uint32_t)lane * ZP_RSTRIDE;
 #pragma unroll
@@ -1003,21 +813,12 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
         wave_lds_fence();
         fv.reg = reg;
     }
-#endif
     Walk w;
     w.rec = zp_rec_full{};
     w.outer = make_uint4(0, 0, 0, 0);
     w.inner = make_uint4(0, 0, 0, 0);
-#ifdef ZP_ABL_FAKE_WALK
-    w.pending = s.live && s.len >= 64;
-    w.l4 = 42; w.acc = 0; w.v6 = 0;
-    w.rec.flags = ZP_F_ETHERNET;
-#else
     bool done = false;
-#if ZP_FAST_V4 || ZP_FAST_IP
     const Probe pr = probe_frame(fv);          // the first header fields, read once
-#endif
-#if ZP_FAST_V4
     // The common shape straight-line when most of the wave has it
     // (wave-uniform test); the rest of the frames take the general walk.
     const bool probe = s.live && v4_probe(fv, pr);
@@ -1025,8 +826,6 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
     if (__builtin_popcountll(__ballot(probe)) >= (SYS ? 1 : 32)) {
         if (probe) done = fast_v4(fv, pr, w);
     }
-#endif
-#if ZP_FAST_IP
     // Mixed stacks straight-line (c5 -5.5 %); what it leaves takes the
     // general walk.
     {
@@ -1035,34 +834,24 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
             if (todo) done = fast_ip(fv, pr, w);
         }
     }
-#endif
     if (__ballot(s.live && !done)) {
         if (s.live && !done) {
             w.rec = zp_rec_full{};
             walk_frame(fv, w);
         }
     }
-#endif
-    STAMP(5);
-    OSTAMP(5);
     if (!s.live) return;
     // The frame's stream sum covers the whole chunks [A & ~15, E16):
     // L4 sum = that - V[A & ~15, A + l4) - V[E, E16).
     zp_rec_full rec = w.rec;
     const uint64_t p = s.tile * 64 + lane;
-#if ZP_EARLY_REC && !defined(ZP_ABL_NOREC)
     // The record as the walk left it goes out before the verdict, so its
     // store's latency overlaps the checksum work instead of ending the wave
     // (two boxes: c5 -1.6 / -0.6 %, c3 -0.3 / +0.6 %, c4 -0.4 / +0.3 %;
     // profiles/r05_kbench_early_rec.log, r05_kbench_early_rec_k2_norec.log);
     // a frame whose L4 checksum then fails stores its error record over it
     // (same lane, same address: the later store lands last).
-#ifdef ZP_REC_PLAIN   // A/B: default-policy record stores
-    if (!SYS) *(zp_u32x2*)(records + p) = zp_pack(rec);
-#else
     if (!SYS) __builtin_nontemporal_store(zp_pack(rec), (zp_u32x2*)(records + p));
-#endif
-#endif
     if (w.pending) {
         bool ok;
         if (s.giant) {
@@ -1070,34 +859,17 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
         } else {
             const bool odd = (s.ga + w.l4) & 1;
             const uint32_t he = (s.len + s.shift) & 15u;    // bytes of the last chunk in use
-#if ZP_REGION
             const uint32_t ex = he ? range_sum(mytail, he, 16u) : 0u;
-#else
-            const uint32_t ex = he ? range_sum(tail[s.rank], he, 16u) : 0u;
-#endif
-#ifdef ZP_ABL_NO_L4HDR
-            ok = csum_ok(w.acc, fsum - ex, odd);                  // timing ablation only
-#else
             ok = csum_ok(w.acc, fsum - sum_to(fv, w.l4) - ex, odd);
-#endif
         }
         if (!ok) {
             rec = zp_rec_full{};
             rec.err = (uint8_t)(w.v6 ? ZP_ERR_IPV6_L4_CHECKSUM : ZP_ERR_IPV4_L4_CHECKSUM);
-#if ZP_EARLY_REC && !defined(ZP_ABL_NOREC)
             if (!SYS) __builtin_nontemporal_store(zp_pack(rec), (zp_u32x2*)(records + p));
-#endif
         }
     }
-    STAMP(6);
-    OSTAMP(6);
     static_assert(sizeof(zp_record) == 8 && sizeof(zp_ext_offsets) == 16, "8-B records");
-#if ZP_EARLY_REC
     if (SYS)
-#endif
-#ifdef ZP_ABL_NOREC
-    if (rec.flags == 0xDEADBEEFu)                       // timing ablation: no stores
-#endif
     {
         // One nontemporal 8-B store per frame: 512 B of whole lines per wave
         // instruction. Writes mixed into the read stream cost several times
@@ -1105,18 +877,12 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
         // arena and the records: nt took 6-7 % off on every
         // placement, 16-B records (v2) 4-6 % against 32-B ones, and 8-B
         // records (v4) 2-7 % more.
-#ifdef ZP_ABL_REC4
-        // Timing probe only (wrong contents): a 4-B record at byte 4 * p
-        const zp_u32x2 q = zp_pack(rec);
-        __builtin_nontemporal_store(q.x ^ q.y, (uint32_t*)records + p);
-#else
         if (SYS) {
             // the server stores it with its acknowledgement (one 16-B store)
             *sys_rec = zp_pack(rec);
         } else {
             __builtin_nontemporal_store(zp_pack(rec), (zp_u32x2*)(records + p));
         }
-#endif
     }
     if (ext) {
         // The extension chains: a wave with at least ZP_EXT_DENSE chains
@@ -1157,62 +923,42 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
 // tiles in dispatch order, so the resident waves always stream a contiguous
 // band of the arena (measured: a persistent grid looping over tiles was
 // 9-12 % slower on c3/c5).
-#ifdef ZP_WPE
 #define ZP_KATTR __launch_bounds__(64 * ZP_WAVES) __attribute__((amdgpu_waves_per_eu(ZP_WPE)))
-#else
-#define ZP_KATTR __launch_bounds__(64 * ZP_WAVES)
-#endif
 // The fused parse + columns kernel carries the column getters too.
-#ifdef ZP_COLS_WPE
-#define ZP_KATTR_COLS __launch_bounds__(64 * ZP_WAVES) __attribute__((amdgpu_waves_per_eu(ZP_COLS_WPE)))
-#else
 #define ZP_KATTR_COLS __launch_bounds__(64 * ZP_WAVES)
-#endif
 // One streamed tile: descriptors given (len, ga), stream, walk, verdict,
 // record store (the batch kernels).
-template <bool COLS, bool TINY = !COLS, class L = WaveLdsParse>
+template <bool COLS, bool TINY = !COLS, class L = WaveLds>
 __device__ __forceinline__ void parse_tile(uint64_t t, uint32_t len, uintptr_t ga, uint64_t n,
                                            int lane, L& lds,
                                            zp_record* __restrict__ records,
                                            zp_ext_offsets* __restrict__ ext,
                                            const ColPtrs& cols) {
-#ifdef ZP_STAMPS
-    const uint64_t wave_id = t;
-#endif
     const uintptr_t fallback = (uintptr_t)&zp_safe_chunk;   // dummy loads when T == 0
     uint4* win = &lds.win[0];
-    uint4* tail = sizeof(lds.win) > sizeof(uint4) * ZP_WIN_CH * 64 ? &lds.win[0] + ZP_WIN_CH * 64
-                                                                  : nullptr;
-#if ZP_TINY
+    uint4* tail = &lds.win[0] + ZP_WIN_CH * 64;
     // a tile of 64-B frames: registers only (wave-uniform test)
     if (TINY && !__ballot(t * 64 + lane < n && len != 64u) &&
         tiny_tile(t, len, ga, n, lane, records))
         return;
-#endif
     TileState s;
     tile_setup(s, t, len, ga, n, lane, lds);
-    STAMP(1);
     // stream: one group of ZP_G items per iteration (group 0 outside the
     // loop, so no load is in flight across the loop back-edge)
-#if ZP_SMALL_G
     if (s.nitems <= ZP_SMALL_G) {              // wave-uniform: a tile of small frames
         // One group of ZP_SMALL_G items holds the whole tile (c2: 4 KiB):
         // no dummy loads past the tile's end (c2 -8 %, c5 -1 %, c3/c4 0).
         uint4 vs[ZP_SMALL_G];
         uint32_t ks[ZP_SMALL_G];
         issue_group<ZP_SMALL_G>(0, s.nitems, s.cur, s.R, lane, fallback, vs, ks);
-        STAMP(2);
         consume_group<ZP_SMALL_G>(0, s.nitems, lane, vs, ks, win, tail, lds.cend, s.run);
     } else
-#endif
     {
     uint4 va[ZP_G];
     uint32_t ka[ZP_G];
     issue_group<ZP_G>(0, s.nitems, s.cur, s.R, lane, fallback, va, ka);
-    STAMP(2);
     consume_group<ZP_G>(0, s.nitems, lane, va, ka, win, tail, lds.cend, s.run);
     for (uint32_t i0 = ZP_G; i0 < s.nitems; i0 += ZP_G) {
-#if ZP_TAIL_G2
         if (s.nitems - i0 <= 2) {                 // the last 1-2 items as a pair
             uint4 vt[2];
             uint32_t kt[2];
@@ -1220,8 +966,6 @@ __device__ __forceinline__ void parse_tile(uint64_t t, uint32_t len, uintptr_t g
             consume_group<2>(i0, s.nitems, lane, vt, kt, win, tail, lds.cend, s.run);
             break;
         }
-#endif
-#if ZP_TAIL_G
         // The last <= ZP_TAIL_G items as a small group: fewer dummy loads
         // past the tile's end, whose address work (4 ds_bpermute each) and
         // consume are not free (c5 -1.7 %, c6 -1.1 %, c3 -0.3 %, c4 0;
@@ -1233,7 +977,6 @@ __device__ __forceinline__ void parse_tile(uint64_t t, uint32_t len, uintptr_t g
             consume_group<ZP_TAIL_G>(i0, s.nitems, lane, vt, kt, win, tail, lds.cend, s.run);
             break;
         }
-#endif
         issue_group<ZP_G>(i0, s.nitems, s.cur, s.R, lane, fallback, va, ka);
         consume_group<ZP_G>(i0, s.nitems, lane, va, ka, win, tail, lds.cend, s.run);
     }
@@ -1248,12 +991,8 @@ __device__ __forceinline__ void parse_tile(uint64_t t, uint32_t len, uintptr_t g
         const uintptr_t org = ((uintptr_t)bperm(s.R.org_hi, r) << 32) | bperm(s.R.org_lo, r);
         s.ga = org + 16ull * bperm(s.R.pfx, r) + s.shift;
     }
-#ifndef ZP_NO_PRIO
     __builtin_amdgcn_s_setprio(0);             // walk at priority 0 ...
-#endif
-    STAMP(3);
     tile_finish<COLS, false, L>(s, n, lane, lds, records, ext, cols);
-    STAMP(4);
 }
 
 template <bool COLS>
@@ -1263,36 +1002,18 @@ __device__ __forceinline__ void parse_tiles(const uint8_t* __restrict__ arena,
                                             zp_record* __restrict__ records,
                                             zp_ext_offsets* __restrict__ ext,
                                             const ColPtrs& cols) {
-    __shared__ WaveLdsParse lds_all[ZP_WAVES];
+    __shared__ WaveLds lds_all[ZP_WAVES];
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
-    WaveLdsParse& lds = lds_all[wid];
+    WaveLds& lds = lds_all[wid];
     // ZP_K consecutive tiles per wave (one contiguous band of the arena)
-#ifdef ZP_SEG
-    // A/B: the grid's blocks interleaved over ZP_SEG contiguous segments of the
-    // batch (a bijection), so the resident waves stream ZP_SEG bands at once.
-    uint64_t blk = blockIdx.x;
-    {
-        const uint64_t B = gridDim.x, S = ZP_SEG, q = B / S, r = B % S;
-        const uint64_t s = blk < S * q ? blk % S : blk - S * q;
-        const uint64_t i = blk < S * q ? blk / S : q;
-        blk = s * q + (s < r ? s : r) + i;
-    }
-#else
     const uint64_t blk = blockIdx.x;
-#endif
     for (uint32_t k = 0; k < ZP_K; ++k) {
         const uint64_t t = (blk * ZP_WAVES + wid) * ZP_K + k;
         if (t * 64 >= n) return;                   // wave-uniform
-#ifdef ZP_STAMPS
-        const uint64_t wave_id = t;
-#endif
-        STAMP(0);
-#ifndef ZP_NO_PRIO
         // ... stream at priority 1: a streaming wave's load issue is not
         // queued behind a walking wave's VALU (c5 +1.8 %, c3/c4 +0-0.5 %)
         __builtin_amdgcn_s_setprio(1);
-#endif
         if (k) wave_lds_fence();                   // previous tile's LDS reads done
         uint32_t len;
         uintptr_t ga;
@@ -1372,21 +1093,21 @@ extern "C" int zp_parse_batch_columns_device(const uint8_t* arena, const uint64_
 // mapped host block: the host writes the frame, then the 64-bit doorbell
 // (sequence << 32 | length); the wave sees it, parses the frame in place as
 // a one-frame tile (parse_tile, the batch kernel's own code), writes the
-// record and the chains back into the block, and then the sequence number
-// into the acknowledgement word. The wave leaves when it has seen no
-// request for `idle` ticks of the 100 MHz constant clock (s_memrealtime) or
-// when the doorbell carries ZP_ONE_STOP, so it never spins past use; the
-// host relaunches it on the next call (zp_ctx.hip: the host knows from its
-// own clock whether the wave may have left, and from the stream whether it
-// did).
+// chains back into the block, and then the record, the sequence number and a
+// tag in one 16-B store. The wave leaves when it has seen no request for
+// `idle` ticks of the 100 MHz constant clock (s_memrealtime), when it has
+// been resident for `life` ticks (1 ms by default, whatever the traffic), or
+// when the doorbell carries ZP_ONE_STOP, so it never spins past use and a
+// device-wide synchronisation never waits longer than its life; the host
+// relaunches it (zp_ctx.hip: the host knows from its own clock when the wave
+// may leave and queues the next one behind it on the same stream).
 // Memory order: the host block is fine-grained (coherent) host memory. The
-// doorbell, the frame bytes (stream and fallback loads) are read with
-// system-scope loads (sc0 sc1, past both caches), so a frame the host
-// rewrote since the last request is never served from a cache and no
-// cache-wide invalidate is needed; the record and chain stores are
-// system-scope (written through), and the wave waits for them to complete
-// before it stores the acknowledgement (guide: "sc0 sc1 stores and loads
-// both sides").
+// doorbell, the acknowledgement read at start and the frame bytes (stream
+// and fallback loads) are read with system-scope loads (sc0 sc1, past both
+// caches), so a frame the host rewrote since the last request is never
+// served from a cache and no cache-wide invalidate is needed; the record and
+// chain stores are system-scope (written through); the chain entries
+// complete inside the tile, before the record store.
 // --------------------------------------------------------------------------
 #define ZP_ONE_BELL 0        // uint64_t: seq << 32 | frame length (host writes)
 #define ZP_ONE_REC 64        // zp_record (server writes) ...
@@ -1395,6 +1116,7 @@ extern "C" int zp_parse_batch_columns_device(const uint8_t* arena, const uint64_
 #define ZP_ONE_EXT 96        // zp_ext_offsets[2] (server writes)
 #define ZP_ONE_FRAME 128     // the frame (host writes)
 #define ZP_ONE_STOP 0xFFFFFFFFu   // doorbell length: leave now
+#define ZP_ONE_TAG 0x9E3779B9u    // answer tag: rec.x ^ rec.y ^ seq ^ ZP_ONE_TAG (zp_ctx.hip)
 
 // The one frame of a zp_parse_one request, streamed by the server wave: its
 // chunks [A & ~15, E) are contiguous, so lane l of item i simply loads chunk
@@ -1448,19 +1170,31 @@ __device__ __forceinline__ void one_frame_tile(uint32_t len, uintptr_t ga, int l
 }
 
 __global__ void __launch_bounds__(64)
-zp_one_server_kernel(uint8_t* blk, uint32_t seq, uint64_t idle) {
+zp_one_server_kernel(uint8_t* blk, uint64_t idle, uint64_t life) {
     __shared__ WaveLds lds;
     const int lane = threadIdx.x & 63;
-#ifdef ZP_ONE_STAMPS   // diagnostic build only (tools/parse_one_latency.py --lib)
-    uint64_t polls = 0;
-#endif
+    // The last answered request is the acknowledgement word in the block (the
+    // previous wave's, or the host's after a stop): a wave queued behind
+    // another never answers a request twice, and answers one rung while it
+    // waited for the stream.
+    uint32_t seq = 0;
+    if (lane == 0)
+        seq = __hip_atomic_load((const uint32_t*)(blk + ZP_ONE_ACK), __ATOMIC_RELAXED,
+                                __HIP_MEMORY_SCOPE_SYSTEM);
+    seq = (uint32_t)__builtin_amdgcn_readlane(seq, 0);
     // One system-scope poll of the doorbell in flight, from lane 0 only
     // (loads of one address from several lanes are not merged and cost
     // ~0.1 us each). Measured and not kept (profiles/r05_parse_one_server_
     // iterations.log): four polling waves (7.2 us per call: they slow the
     // working wave's host accesses), and several polls in flight from this
     // wave (the compiler waits for all of them at the rotation's head).
-    uint64_t last = __builtin_amdgcn_s_memrealtime();
+    // The wave leaves after `idle` ticks without a request and, whatever the
+    // traffic, once it has been resident for `life` ticks: a device-wide
+    // synchronisation issued meanwhile (hipDeviceSynchronize,
+    // torch.cuda.synchronize, hipFree) waits at most that long. The host
+    // relaunches it behind the old one on the same stream (zp_ctx.hip).
+    const uint64_t born = __builtin_amdgcn_s_memrealtime();
+    uint64_t last = born;
     for (;;) {
         uint64_t bell = 0;
         if (lane == 0)
@@ -1469,19 +1203,14 @@ zp_one_server_kernel(uint8_t* blk, uint32_t seq, uint64_t idle) {
         const uint32_t bseq = (uint32_t)__builtin_amdgcn_readlane((uint32_t)(bell >> 32), 0);
         const uint32_t blen = (uint32_t)__builtin_amdgcn_readlane((uint32_t)bell, 0);
         if (bseq == seq) {
-            if (__builtin_amdgcn_s_memrealtime() - last > idle) break;
+            const uint64_t now = __builtin_amdgcn_s_memrealtime();
+            if (now - last > idle || now - born > life) break;
+            __builtin_amdgcn_s_sleep(1);                     // ~64 clocks between polls
             continue;
         }
         if (blen == ZP_ONE_STOP) break;
         seq = bseq;
-#ifdef ZP_ONE_STAMPS
-        ++polls;
-#endif
         {                                                    // a request (wave-uniform)
-#ifdef ZP_ONE_STAMPS
-            const uint64_t t_bell = __builtin_amdgcn_s_memrealtime();
-            const uint64_t c_bell = __builtin_amdgcn_s_memtime();
-#endif
             __builtin_amdgcn_s_setprio(1);
             // every load of the frame and every store of the results is
             // system-scope (SYS): nothing is left in a cache to invalidate
@@ -1490,40 +1219,48 @@ zp_one_server_kernel(uint8_t* blk, uint32_t seq, uint64_t idle) {
             one_frame_tile(blen, (uintptr_t)(blk + ZP_ONE_FRAME), lane, lds,
                            (zp_record*)(blk + ZP_ONE_REC), (zp_ext_offsets*)(blk + ZP_ONE_EXT),
                            (uintptr_t)blk, &rec);
-#ifdef ZP_ONE_STAMPS
-            const uint64_t t_tile = __builtin_amdgcn_s_memrealtime();
-            const uint64_t c_tile = __builtin_amdgcn_s_memtime();
-#endif
-#ifdef ZP_ONE_STAMPS
-            if (lane == 0) {
-                st_sys8(blk + 32, t_bell);
-                st_sys8(blk + 40, t_tile);
-                st_sys8(blk + 48, __builtin_amdgcn_s_memrealtime());
-                st_sys8(blk + 56, polls);
-                st_sys8(blk + 24, c_tile - c_bell);
-            }
-            polls = 0;
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
-            // The record and the acknowledgement in one 16-B store: the host
-            // sees both at once, so nothing waits for the record's completion
-            // first (a host-link round trip, ~1.2 us; the chain entries,
-            // when there are any, completed inside the tile).
+            // The record and the acknowledgement in one 16-B store, so
+            // nothing waits for the record's completion first (a host-link
+            // round trip, ~1.2 us; the chain entries, when there are any,
+            // completed inside the tile). The fourth word tags the record
+            // with the seq (ZP_ONE_TAG): the host accepts the answer only
+            // when ack and tag agree with the record it read, so a 16-B
+            // write the host link delivered in pieces is waited out, not
+            // returned.
             if (lane == 0)
-                st_sys16((uintptr_t)blk, (uintptr_t)(blk + ZP_ONE_REC), zp_u32x4{rec.x, rec.y, bseq, 0u});
+                st_sys16((uintptr_t)blk, (uintptr_t)(blk + ZP_ONE_REC),
+                         zp_u32x4{rec.x, rec.y, bseq, rec.x ^ rec.y ^ bseq ^ ZP_ONE_TAG});
             wave_lds_fence();                                 // LDS reused by the next request
+            __builtin_amdgcn_s_setprio(0);                    // polls at the base priority
             last = __builtin_amdgcn_s_memrealtime();
+            if (last - born > life) break;
         }
     }
 }
 
 extern "C" __attribute__((visibility("hidden"))) int zp__one_server_launch(uint8_t* blk_d,
-                                                                            uint32_t seq,
                                                                             uint64_t idle_ticks,
+                                                                            uint64_t life_ticks,
                                                                             void* stream) {
     hipLaunchKernelGGL(zp_one_server_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, blk_d,
-                       seq, idle_ticks);
+                       idle_ticks, life_ticks);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) { set_err("zp_one_server_kernel launch", e); return -2; }
+    return 0;
+}
+
+// Test hook (zp__one_test_hooks, zp_ctx.hip): one wave that spins for `ticks`
+// of the constant clock, queued in front of a server launch to make the
+// server start late.
+__global__ void __launch_bounds__(64) zp_one_stall_kernel(uint64_t ticks) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
+extern "C" __attribute__((visibility("hidden"))) int zp__one_stall_launch(uint64_t ticks,
+                                                                           void* stream) {
+    hipLaunchKernelGGL(zp_one_stall_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, ticks);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) { set_err("zp_one_stall_kernel launch", e); return -2; }
     return 0;
 }

@@ -15,9 +15,7 @@
 // descriptor (KEEP_WIN): at most 16 chunks.
 static_assert(ZP_WIN % 16 == 0 && ZP_WIN <= 256, "ZP_WIN must be a multiple of 16, <= 256");
 #define ZP_GIANT 65536u      // frames longer than this take the exact path
-#ifndef ZP_G
 #define ZP_G 8               // stream items (1 KiB loads) per group
-#endif
 
 // All loads go through address_space(1) pointers: pointers rebuilt from
 // integers would otherwise compile to FLAT loads, which count against both
@@ -99,19 +97,14 @@ __device__ __forceinline__ uint32_t chunk_sum(uint4 v, int l, int h, uint32_t s)
 // (2^16 == 1 mod 65535; the second fold leaves 1..65535 for x != 0) instead of
 // a 32-bit modulo (a multiply-high sequence).
 __device__ __forceinline__ bool nz_mod65535_zero(uint32_t x) {
-#ifdef ZP_CSUM_MOD
-    return x != 0 && x % 65535u == 0;        // A/B: the modulo form
-#else
     const uint32_t y = (x & 0xFFFFu) + (x >> 16);
     return x != 0 && (y & 0xFFFFu) + (y >> 16) == 65535u;
-#endif
 }
 
 // Checksum validity from the arena-parity sum V of a segment starting at an
 // address of parity `odd`, with accumulator acc (fast path, exact V).
 __device__ __forceinline__ bool csum_ok(uint32_t acc, uint32_t V, bool odd) {
     if (acc == 0 && V == 0) return false;                  // S == 0 -> 0xFFFF
-#ifndef ZP_CSUM_MOD
     // 2^16 == 1 (mod 65535): t = acc + W folded by 16-bit limbs (t < 2^41);
     // t > 0 here, so t == 0 (mod 65535) iff the folds end at 65535 (the
     // modulo form below checked against it on 4M random and edge inputs;
@@ -121,11 +114,6 @@ __device__ __forceinline__ bool csum_ok(uint32_t acc, uint32_t V, bool odd) {
     x = (x & 0xFFFFu) + (x >> 16);
     x = (x & 0xFFFFu) + (x >> 16);
     return x == 65535u;
-#else
-    uint32_t w = V % 65535u;
-    if (!odd) w = (w * 256u) % 65535u;
-    return ((acc % 65535u) + w) % 65535u == 0;
-#endif
 }
 
 // --------------------------------------------------------------------------
@@ -202,9 +190,7 @@ struct Ranked {          // lane r = frame of rank r
 #define KEEP_IN (1u << 31)     // chunk belongs to a frame (else past the end)
 #define KEEP_WIN (1u << 30)    // chunk index < ZP_WIN_CH: window cell in bits 0-9
 #define KEEP_TAIL (1u << 29)   // frame's last chunk
-#ifndef ZP_T4N
 #define ZP_T4N 3               // chunks kept before each frame's last one (T4 streams, <= 3)
-#endif
 #define KEEP_T4 (1u << 28)     // one of the ZP_T4N chunks before the frame's last (T4 streams) ...
 #define KEEP_T4D(k) (((k) >> 22) & 3u)   // ... at this distance from the last, minus 1
 #define KEEP_MID (1u << 27)    // (T4 streams) the chunk of the frame's marked offset, its byte in 10-13
@@ -216,9 +202,7 @@ __device__ __forceinline__ uint32_t bperm(uint32_t v, uint32_t r) {
     return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(r << 2), (int)v);
 }
 
-#ifndef ZP_STARTS
 #define ZP_STARTS 64           // items per rebuild of the frame-start masks (a power of two >= ZP_G)
-#endif
 // Rebuilds the start masks of items [w0, w0 + ZP_STARTS): one LDS atomic OR per
 // frame starting there. Straight-line code (no loop): a loop here would make
 // LLVM's wait-count insertion drain the group in flight (vmcnt(0)).
@@ -245,7 +229,6 @@ __device__ __forceinline__ void issue_group(uint32_t i0, uint32_t nitems, Cursor
                                             const Ranked& R, int lane, uintptr_t fallback,
                                             uint4 (&v)[G], uint32_t (&keep)[G]) {
     uintptr_t a[G];
-#ifndef ZP_FMASK_ITEM
     // The G items' frame-start masks in one LDS round trip (G divides 64, so
     // the group never straddles a rebuild of the mask table).
     static_assert(ZP_STARTS % G == 0 && G % 2 == 0 && ZP_STARTS <= 64,
@@ -266,22 +249,11 @@ __device__ __forceinline__ void issue_group(uint32_t i0, uint32_t nitems, Cursor
                             (uint32_t)__builtin_amdgcn_readfirstlane(lo);
         Fq[q] = i0 + q < nitems ? fu : 0ull;
     }
-#endif
 #pragma unroll
     for (int q = 0; q < G; ++q) {
         const uint32_t i = i0 + q;
         const uint32_t base = 64u * i;
-#ifdef ZP_FMASK_ITEM
-        if ((i & (ZP_STARTS - 1u)) == 0 && i < nitems) build_starts(i, c, R, lane);   // wave-uniform
-        uint64_t F = 0;
-        if (i < nitems) {
-            const uint64_t f = c.starts[i & (ZP_STARTS - 1u)];
-            F = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(f >> 32)) << 32) |
-                (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)f);
-        }
-#else
         const uint64_t F = Fq[q];
-#endif
         const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(F >> 32),
                                    __builtin_amdgcn_mbcnt_lo((uint32_t)F, 0u));
         uint32_t r = c.rbase + below + (uint32_t)((F >> lane) & 1u);
@@ -303,10 +275,8 @@ __device__ __forceinline__ void issue_group(uint32_t i0, uint32_t nitems, Cursor
         const uint32_t vc = vv < lv ? vv : lv;
         a[q] = nitems ? (((uintptr_t)ohi << 32) | olo) + 16ull * vc : fallback;
     }
-#ifndef ZP_ABL_STREAM_OFF
 #pragma unroll
     for (int q = 0; q < G; ++q) v[q] = ld_stream(a[q]);
-#endif
     // Compiler barrier: keeps LLVM from sinking the loads below the consume
     // of the previous group (which would serialise the double buffer).
     asm volatile("" ::: "memory");
@@ -342,15 +312,7 @@ __device__ __forceinline__ void consume_group(uint32_t i0, uint32_t nitems, int 
         part = sad16(v[q].y, part);
         part = sad16(v[q].z, part);
         part = sad16(v[q].w, part);
-#ifdef ZP_ABL_NOSCAN
-        const uint32_t P = k & KEEP_IN ? part : 0u;           // timing ablation only
-#else
         const uint32_t P = wave_scan(k & KEEP_IN ? part : 0u);
-#endif
-#ifdef ZP_ABL_EXTRA
-#pragma unroll
-        for (int x = 0; x < ZP_ABL_EXTRA; ++x) asm volatile("v_add_u32 %0, %0, 1" : "+v"(part));
-#endif
         if (k & KEEP_TAIL) {
             if (tail != nullptr) tail[KEEP_RANK(k)] = v[q];
             cend[KEEP_RANK(k)] = run + P;
@@ -369,25 +331,11 @@ __device__ __forceinline__ void consume_group(uint32_t i0, uint32_t nitems, int 
 // The batch kernel.
 // --------------------------------------------------------------------------
 // One tile = 64 consecutive frames on one wave (lane = frame).
-template <int TAILS>
-struct WaveLdsT {
-    uint4 win[(ZP_WIN_CH + TAILS) * 64];   // header windows [ZP_WIN_CH][64] (+ last chunks [64])
+struct WaveLds {
+    uint4 win[(ZP_WIN_CH + 1) * 64];   // header windows [ZP_WIN_CH][64] (+ last chunks [64])
     uint32_t cend[64];                      // running stream sum at each frame's last chunk
     uint64_t starts[ZP_STARTS];             // per-item frame-start masks
 };
-// With the last chunk of every frame (the builder, the zp_parse_one server).
-typedef WaveLdsT<1> WaveLds;
-// The parse kernels' layout. ZP_NO_TAIL (A/B, with ZP_STARTS 32): no
-// last-chunk cells; the bytes past a frame's end come from the next rank's
-// first window cell (the same 16-B chunk when frames lie back to back) or
-// from memory, so a wave needs 7.5 KiB and a CU holds 21 waves instead of 18
-// (profiles/r05_lds_residency.log). Byte-exact (GPU suite green with it) but
-// within +-1 % on every config on two boxes
-// (profiles/r05_kbench_tail_free_layout.log): off.
-#ifndef ZP_NO_TAIL
-#define ZP_NO_TAIL 0
-#endif
-typedef WaveLdsT<ZP_NO_TAIL ? 0 : 1> WaveLdsParse;
 
 struct TileState {
     uint64_t tile;

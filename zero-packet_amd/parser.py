@@ -557,17 +557,23 @@ class PacketParser:
 
     @classmethod
     def parse(cls, frame):
-        """PacketParser::parse (parser.rs:53) through the GPU path."""
+        """PacketParser::parse (parser.rs:53) through the GPU path, on the
+        calling thread's current HIP device. Reentrant like the reference's
+        pure parse: each call takes a context of its own from the device's
+        pool (a zp_ctx serves one call at a time), so threads run their
+        calls concurrently."""
         frame = bytes(frame)
         rec = np.zeros(1, RECORD_DTYPE)
         ext = np.zeros(2, EXT_DTYPE)
         buf = ctypes.create_string_buffer(frame, len(frame) or 1)
-        # The shared zp_ctx (pinned staging, device buffers, streams) serves one
-        # call at a time; ctypes releases the GIL, so callers on other threads
-        # wait here (the reference's parse is pure and thread-safe).
-        with _CTX_LOCK:
-            rc = _lib.hip().zp_parse_one(_default_ctx(), ctypes.addressof(buf), len(frame),
-                                         rec.ctypes.data, ext.ctypes.data)
+        lib = _lib.hip()
+        dev = lib.zp_device_current()
+        if dev < 0:
+            raise RuntimeError("zp_device_current failed: " + lib.zp_last_error().decode())
+        pool = _pool(dev)
+        with pool.context(len(frame)) as ctx:
+            rc = lib.zp_parse_one(ctx, ctypes.addressof(buf), len(frame),
+                                  rec.ctypes.data, ext.ctypes.data)
         _lib.check(rc, "zp_parse_one")
         return cls.from_record(frame, rec[0], ext)
 
@@ -580,26 +586,119 @@ def _lib_available():
         return False
 
 
-_CTX = None
-_CTX_LOCK = threading.Lock()
+ONE_MAX = 64 << 10          # zp_parse_one's mapped-block frame limit (zp_ctx.hip ONE_MAX)
+POOL_CHUNK = 1 << 20        # chunk size of a pooled context (frames <= ONE_MAX only)
+POOL_MAX = 32               # pooled contexts per device; more callers wait for one
 
 
-def _default_ctx():
-    """The module's zp_ctx; callers hold _CTX_LOCK."""
-    global _CTX
-    if _CTX is None:
-        _CTX = _lib.hip().zp_ctx_create(0, 0)
-        if not _CTX:
-            raise RuntimeError("zp_ctx_create failed: " + _lib.hip().zp_last_error().decode())
-        atexit.register(quiesce)
-    return _CTX
+class _DevicePool:
+    """zp_ctx pool of one device. Frames up to ONE_MAX take a small pooled
+    context each (its own mapped block and resident server wave, so calls on
+    different threads never wait for each other); longer frames take the
+    device's one large context (256 MiB chunks) under a lock."""
+
+    def __init__(self, device):
+        self.device = device
+        self.cv = threading.Condition()
+        self.free = []
+        self.all = []
+        self.big = None
+        self.big_lock = threading.Lock()
+
+    def _create(self, chunk):
+        lib = _lib.hip()
+        ctx = lib.zp_ctx_create(self.device, chunk)
+        if not ctx:
+            raise RuntimeError("zp_ctx_create failed: " + lib.zp_last_error().decode())
+        return ctx
+
+    def _take(self):
+        with self.cv:
+            while not self.free and len(self.all) >= POOL_MAX:
+                self.cv.wait()
+            if self.free:
+                return self.free.pop()          # LIFO: the context whose server is warm
+            self.all.append(None)               # reserve a slot, create outside the lock
+        try:
+            ctx = self._create(POOL_CHUNK)
+        except Exception:
+            with self.cv:
+                self.all.remove(None)
+                self.cv.notify()
+            raise
+        with self.cv:
+            self.all[self.all.index(None)] = ctx
+        return ctx
+
+    def _give(self, ctx):
+        with self.cv:
+            self.free.append(ctx)
+            self.cv.notify()
+
+    class _Lease:
+        def __init__(self, pool, big):
+            self.pool, self.big, self.ctx = pool, big, None
+
+        def __enter__(self):
+            p = self.pool
+            if self.big:
+                p.big_lock.acquire()
+                try:
+                    if p.big is None:
+                        p.big = p._create(0)
+                except Exception:
+                    p.big_lock.release()
+                    raise
+                self.ctx = p.big
+            else:
+                self.ctx = p._take()
+            return self.ctx
+
+        def __exit__(self, *exc):
+            if self.big:
+                self.pool.big_lock.release()
+            else:
+                self.pool._give(self.ctx)
+            return False
+
+    def context(self, nbytes):
+        """A lease on a context for one call on a frame of nbytes."""
+        return _DevicePool._Lease(self, nbytes > ONE_MAX)
+
+    def quiesce(self):
+        """Stops the servers of the contexts no call holds (a held one's
+        server leaves within its 1 ms life anyway)."""
+        lib = _lib.hip()
+        with self.cv:
+            for ctx in self.free:
+                lib.zp_parse_one_config(ctx, 5000)
+        with self.big_lock:
+            if self.big is not None:
+                lib.zp_parse_one_config(self.big, 5000)
+
+
+_POOLS = {}
+_POOLS_LOCK = threading.Lock()
+
+
+def _pool(device):
+    """The context pool of `device` (created on first use)."""
+    with _POOLS_LOCK:
+        p = _POOLS.get(device)
+        if p is None:
+            if not _POOLS:
+                atexit.register(quiesce)
+            p = _POOLS[device] = _DevicePool(device)
+        return p
 
 
 def quiesce():
-    """Stops the default context's resident zp_parse_one server wave now
-    (it also leaves by itself after 5 ms without a call; the next
-    PacketParser.parse relaunches it). Call before a device-wide
-    synchronisation to avoid waiting for that timeout."""
-    with _CTX_LOCK:
-        if _CTX is not None:
-            _lib.hip().zp_parse_one_config(_CTX, 5000)
+    """Stops the resident zp_parse_one server waves of every idle context now
+    (each also leaves by itself after 5 ms without a call, and after 1 ms
+    resident whatever the traffic; the next PacketParser.parse relaunches
+    it). Call before a device-wide synchronisation to avoid waiting for
+    that bound."""
+    with _POOLS_LOCK:
+        pools = list(_POOLS.values())
+    for p in pools:
+        p.quiesce()
