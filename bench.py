@@ -29,9 +29,10 @@ Reported next to the GPU number:
                 a 2M-frame sample (zp_parse_batch_host), every rank at once,
                 frames summed over ranks / the slowest rank; never `value`;
                 rejected frames reported, not asserted
-  roofline.placement  a plain streaming read of the same arena (the
-                placement class: the parse's rate moves with the arena's
-                physical pages, DESIGN.md §4, and a pure read moves with it)
+  roofline.placement  the placement classes of the bench's own buffers: a
+                plain streaming read of the arena, the parse's tile pattern
+                over it, and that pattern with the 8-B record stores into the
+                bench's records buffer
   config5       BASELINE config 5 in the same ranks after the headline: the
                 256M-frame IMIX stream (--c5-frames) cut into N contiguous
                 shards (strong scaling), its own timed loop of --steps
@@ -204,33 +205,54 @@ def pcie_inclusive(zp, arena, offs, lens, sample_pkts, barrier=lambda: None):
 PCIE_PATH = "pinned host -> H2D -> kernel -> D2H records, 2 streams x 256 MiB chunks"
 
 
-def placement_probe(zp, arena, kernel_ms, reps=5):
-    """The arena's placement class, measured: a plain streaming read of the
-    whole arena (zp_probe_read_device, HIP events on the launch stream) beside
-    the parse. Copies of one arena in different allocations parse at 0.77 /
-    0.80 / 0.82 of peak (the physical pages decide); a pure read
-    moves with them, so two lines of identical code on different placements
-    are told apart by read_gbs and parse_over_read."""
+def placement_probe(zp, arena, n, records, kernel_ms, reps=5):
+    """The placement classes of the bench's own buffers, measured beside the
+    parse on the launch stream (HIP events, interleaved rounds, medians):
+      read      a plain grid-stride streaming read of the whole arena
+                (zp_probe_read_device): the arena's placement;
+      tiles     the parse's tile pattern, reads only (zp_probe_tiles_device:
+                one wave per 64-frame slice, a parse wave's LDS);
+      tiles_rec the same plus the 8-B record stores into the bench's records
+                buffer: tiles_rec - tiles is what the record stores cost on
+                this records placement.
+    parse_over_* = the parse kernel's mean time / the probe's."""
     import ctypes
     lib = zp._lib.hip()
     sink = torch.zeros(1, dtype=torch.int32, device=arena.device)
     stream = torch.cuda.current_stream(arena.device)
     nb = arena.numel() // 16 * 16
     s = ctypes.c_void_p(stream.cuda_stream)
-    zp._lib.check(lib.zp_probe_read_device(arena.data_ptr(), nb, sink.data_ptr(), s), "probe")
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(reps)]
-    for a, b in ev:
-        a.record(stream)
-        lib.zp_probe_read_device(arena.data_ptr(), nb, sink.data_ptr(), s)
-        b.record(stream)
+    probes = {
+        "read": lambda: lib.zp_probe_read_device(arena.data_ptr(), nb, sink.data_ptr(), s),
+        "tiles": lambda: lib.zp_probe_tiles_device(arena.data_ptr(), nb, n, None,
+                                                   sink.data_ptr(), s),
+        "tiles_rec": lambda: lib.zp_probe_tiles_device(arena.data_ptr(), nb, n,
+                                                       records.data_ptr(), sink.data_ptr(), s),
+    }
+    for f in probes.values():
+        zp._lib.check(f(), "placement probe")
+    ms = {k: [] for k in probes}
+    for _ in range(reps):
+        for k, f in probes.items():
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+            f()
+            b.record(stream)
+            ms[k].append((a, b))
     torch.cuda.synchronize()
-    ms = float(np.median([a.elapsed_time(b) for a, b in ev]))
-    return {"arena_bytes": nb, "read_ms": round(ms, 4),
-            "read_gbs": round(nb / (ms * 1e-3) / 1e9, 1),
-            "parse_over_read": round(kernel_ms / ms, 4),
+    med = {k: float(np.median([a.elapsed_time(b) for a, b in v])) for k, v in ms.items()}
+    return {"arena_bytes": nb, "read_ms": round(med["read"], 4),
+            "read_gbs": round(nb / (med["read"] * 1e-3) / 1e9, 1),
+            "tiles_ms": round(med["tiles"], 4), "tiles_rec_ms": round(med["tiles_rec"], 4),
+            "record_store_ms": round(med["tiles_rec"] - med["tiles"], 4),
+            "parse_over_read": round(kernel_ms / med["read"], 4),
+            "parse_over_tiles": round(kernel_ms / med["tiles"], 4),
+            "parse_over_tiles_rec": round(kernel_ms / med["tiles_rec"], 4),
             "arena_va_mod_1g": arena.data_ptr() % (1 << 30),
-            "probe": "zp_probe_read_device: grid-stride nt 16-B loads, 2048 x 256 lanes"}
+            "records_va_mod_1g": records.data_ptr() % (1 << 30),
+            "probe": "zp_probe_read_device: grid-stride nt 16-B loads, 2048 x 256 lanes; "
+                     "zp_probe_tiles_device: one wave per 64-frame slice, nt 16-B loads, "
+                     "tiles_rec + 64 nt 8-B stores per wave into the bench's records"}
 
 
 def gather_rows(row, world, rank, dev):
@@ -424,7 +446,7 @@ def main():
                      "algorithmic_bytes_per_launch": total_bytes},
     }
     coll_dev = "cpu" if shared else dev
-    out["roofline"]["placement"] = placement_probe(zp, arena, kmean)
+    out["roofline"]["placement"] = placement_probe(zp, arena, n, records, kmean)
     if not args.no_pcie:
         # every rank's host path at once: frames of all ranks / the slowest rank
         m, nb, sec, perr = pcie_inclusive(zp, arena, offs, lens, 1 << 21, barrier)

@@ -170,9 +170,10 @@ def test_gpu_columns_vs_oracle(zp, golden, case):
     for name in ("src_port", "dest_addr"):
         assert np.array_equal(sub[name].cpu().numpy(), want[name])
     # parse_with_columns gives the same records and columns on every path:
-    # the fused pass, parse + extract, and "auto" while it times both (the
-    # first call of a workload) and after it has chosen
-    for mode in ["fused", "split", "auto", "auto"]:
+    # the fused pass, parse + extract, and "auto" while it alternates and
+    # times both (the first calls of a workload) and after it has chosen
+    zp.columns.reset_auto()                             # this traffic: a fresh workload
+    for mode in ["fused", "split"] + ["auto"] * 7:
         frecs, _, fcols = zp.columns.parse_with_columns(a, o, l_, mode=mode)
         fsub = zp.columns.parse_with_columns(a, o, l_, names=["tcp_seq", "vlan_tci"],
                                              mode=mode)[2]

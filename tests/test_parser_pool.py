@@ -55,9 +55,10 @@ def fake(zp, monkeypatch):
     P = zp.parser
     lib = FakeLib()
     monkeypatch.setattr(zp._lib, "hip", lambda: lib)
+    monkeypatch.setattr(zp._lib, "pyhip", lambda: lib)
     monkeypatch.setattr(P, "_POOLS", {})
-    monkeypatch.setattr(P.PacketParser, "from_record",
-                        classmethod(lambda cls, f, r, x: ("ok", len(f))))
+    monkeypatch.setattr(P.PacketParser, "_from_words",
+                        classmethod(lambda cls, f, w, o, x: ("ok", len(f))))
     return lib
 
 
@@ -113,11 +114,11 @@ def test_quiesce_touches_idle_contexts_only(zp, fake):
     P = zp.parser
     P.PacketParser.parse(b"\0" * 64)
     pool = P._POOLS[0]
-    held = pool._take()                                    # a call in flight elsewhere
+    held = pool.take()                                    # a call in flight elsewhere
     P.quiesce()
     assert held not in fake.configured
     assert set(fake.configured) == set(pool.free)
-    pool._give(held)
+    pool.give(held)
 
 
 def test_device_error_raises(zp, fake):
@@ -125,3 +126,34 @@ def test_device_error_raises(zp, fake):
     fake.device = -1
     with pytest.raises(RuntimeError):
         P.PacketParser.parse(b"\0" * 64)
+
+
+def test_fast_record_path_equals_from_record(zp, golden):
+    """PacketParser.parse rebuilds the common record (ordinary form, no
+    extension chain) without from_record's general decode; on the golden
+    packets and every config's frames both give the same parser (Debug
+    text) or the same error."""
+    import ctypes
+    import oracle as orc
+    P = zp.parser.PacketParser
+    frames = [bytes.fromhex(fx["bytes"]) for fx in golden["fixtures"]]
+    for c in ("c1", "c3", "c4", "c5", "c6"):
+        a, o, l_ = zp.batch.generate_host(c, 800, first=77)
+        frames += [a[int(x):int(x) + int(y)].tobytes() for x, y in zip(o, l_)]
+
+    def res(fn):
+        try:
+            return fn().debug()
+        except zp.parser.ZeroPacketError as e:
+            return repr(e)
+    kinds = set()
+    for f in frames:
+        err, r, x = orc.parse_one(f)
+        pr = orc.pack(r, x)[0]
+        ext = (ctypes.c_uint8 * 32)()
+        ctypes.memmove(ext, x.tobytes(), 32)
+        w, o = int(pr["flags"]), int(pr["offs"])
+        kinds.add(bool(w >> 26 or w & (zp.records.F_EXT | zp.records.F_INNER_EXT)))
+        assert res(lambda: P.from_record(f, pr, x)) == res(lambda: P._from_words(f, w, o, ext)), \
+            f.hex()
+    assert kinds == {False, True}                      # both paths were exercised

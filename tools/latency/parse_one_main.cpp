@@ -1,13 +1,14 @@
 // Per-frame latency of zp_parse_one (PacketParser::parse for one frame,
 // parser.rs:53, through the GPU: H2D -> kernel -> D2H -> sync), the drop-in
 // for a caller that parses frame by frame. stdin: frame hex lines.
-//   parse_one_main <threads> <calls per thread> [idle_us]
+//   parse_one_main <threads> <calls per thread> [idle_us] [life_us]
 // idle_us: zp_parse_one's mode (zp_parse_one_config): > 0 the resident server
 // wave with that idle timeout (default 5000), 0 one kernel launch per call.
 // Each thread owns one zp::Context (a zp_ctx may not be shared) and parses
 // the frames round robin; prints mean / p50 / p99 microseconds per call and
 // the aggregate calls per second.
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <iostream>
@@ -19,11 +20,16 @@
 
 // diagnostic builds (-DZP_ONE_STAMPS) export the server's in-kernel stamps
 extern "C" void zp__one_stamps(zp_ctx*, uint64_t*) __attribute__((weak));
+// test hooks of libzp_hip.so: the server's life, its counters
+extern "C" int zp__one_test_hooks(zp_ctx*, uint32_t, uint64_t, uint32_t) __attribute__((weak));
+extern "C" int zp__one_stats(const zp_ctx*, uint64_t*) __attribute__((weak));
 
 int main(int argc, char** argv) {
     const int threads = argc > 1 ? std::atoi(argv[1]) : 1;
     const int calls = argc > 2 ? std::atoi(argv[2]) : 2000;
     const uint32_t idle_us = argc > 3 ? (uint32_t)std::atoi(argv[3]) : 5000u;
+    const uint32_t life_us = argc > 4 ? (uint32_t)std::atoi(argv[4]) : 0u;   // 0: the default
+    std::vector<uint64_t> stats(3 * threads, 0);
     std::vector<std::vector<uint8_t>> frames;
     std::string line;
     while (std::getline(std::cin, line)) {
@@ -34,12 +40,21 @@ int main(int argc, char** argv) {
     std::vector<std::vector<double>> lat(threads);
     std::vector<int> bad(threads, 0);
     std::vector<double> busy(threads, 0);
+    // every thread's timed loop starts together (after its context and
+    // warm-up) and the rate is the calls over the span from the common
+    // start to the last thread's end
+    std::atomic<int> ready{0};
+    std::vector<std::chrono::steady_clock::time_point> t_end(threads);
+    std::chrono::steady_clock::time_point t_start;
     std::vector<std::vector<double>> st(5), ph(8);    // thread 0: bell->tile, tile->stores done, polls
     auto worker = [&](int t) {
         zp::Context ctx(0);
         ctx.parse_one_mode(idle_us);
+        if (life_us && zp__one_test_hooks) zp__one_test_hooks(ctx.get(), life_us, 0, 0);
         for (int w = 0; w < 50; ++w) ctx.parse(zp::Bytes{frames[0].data(), frames[0].size()});
         lat[t].reserve(calls);
+        if (ready.fetch_add(1) + 1 == threads) t_start = std::chrono::steady_clock::now();
+        while (ready.load() < threads) {}
         const auto tb = std::chrono::steady_clock::now();
         for (int k = 0; k < calls; ++k) {
             const auto& f = frames[(k + t) % frames.size()];
@@ -60,13 +75,20 @@ int main(int argc, char** argv) {
             }
             lat[t].push_back(std::chrono::duration<double, std::micro>(t1 - t0).count());
         }
-        busy[t] = std::chrono::duration<double>(std::chrono::steady_clock::now() - tb).count();
+        t_end[t] = std::chrono::steady_clock::now();
+        busy[t] = std::chrono::duration<double>(t_end[t] - tb).count();
+        if (zp__one_stats) zp__one_stats(ctx.get(), &stats[3 * t]);
     };
     std::vector<std::thread> th;
     for (int t = 0; t < threads; ++t) th.emplace_back(worker, t);
     for (auto& x : th) x.join();
-    double wall = 0;             // the timed loops (context creation and warm-up excluded)
-    for (double b : busy) wall = b > wall ? b : wall;
+    // the concurrent span of the timed loops (context creation and warm-up
+    // excluded): common start to the last thread's end
+    double wall = 0;
+    for (int t = 0; t < threads; ++t) {
+        const double w = std::chrono::duration<double>(t_end[t] - t_start).count();
+        wall = w > wall ? w : wall;
+    }
     std::vector<double> all;
     for (auto& v : lat) all.insert(all.end(), v.begin(), v.end());
     std::sort(all.begin(), all.end());
@@ -74,10 +96,15 @@ int main(int argc, char** argv) {
     for (double x : all) sum += x;
     int nbad = 0;
     for (int b : bad) nbad += b;
-    std::printf("{\"idle_us\": %u, \"threads\": %d, \"calls\": %zu, \"mean_us\": %.2f, \"p50_us\": %.2f, "
-                "\"p99_us\": %.2f, \"calls_per_s\": %.0f, \"rejected\": %d}\n",
-                idle_us, threads, all.size(), sum / all.size(), all[all.size() / 2],
-                all[(size_t)(all.size() * 0.99)], all.size() / wall, nbad);
+    uint64_t tot[3] = {0, 0, 0};
+    for (int t = 0; t < threads; ++t)
+        for (int k = 0; k < 3; ++k) tot[k] += stats[3 * t + k];
+    std::printf("{\"idle_us\": %u, \"life_us\": %u, \"threads\": %d, \"calls\": %zu, \"mean_us\": %.2f, "
+                "\"p50_us\": %.2f, \"p99_us\": %.2f, \"calls_per_s\": %.0f, \"rejected\": %d, "
+                "\"max_us\": %.1f, \"server_launches_rotations_relaunches\": [%llu, %llu, %llu]}\n",
+                idle_us, life_us, threads, all.size(), sum / all.size(), all[all.size() / 2],
+                all[(size_t)(all.size() * 0.99)], all.size() / wall, nbad, all.back(),
+                (unsigned long long)tot[0], (unsigned long long)tot[1], (unsigned long long)tot[2]);
     if (!st[0].empty()) {
         for (auto& v : st) std::sort(v.begin(), v.end());
         std::printf("{\"server_stamps_p50\": {\"bell_to_tile_us\": %.2f, \"tile_to_stores_done_us\": %.2f, "

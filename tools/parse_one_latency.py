@@ -27,6 +27,7 @@ def main():
                     help="zp_parse_one_config idle_us per run: >0 resident server, 0 launch per call")
     ap.add_argument("--lib", default="", help="directory of another libzp_hip.so build (A/B)")
     ap.add_argument("--py-threads", default="1,8", help="Python facade thread counts ('' = skip)")
+    ap.add_argument("--lives", default="0", help="server life per run in us (test hook; 0 = default)")
     args = ap.parse_args()
     zp = importlib.import_module("zero-packet_amd")
     a, o, l_ = zp.batch.generate_host("c3", 256)
@@ -36,9 +37,11 @@ def main():
     subprocess.run(["g++", "-std=c++17", "-O2", "-pthread", "-I", os.path.join(ROOT, "include"),
                     "-o", exe, os.path.join(ROOT, "tools", "latency", "parse_one_main.cpp"),
                     "-L" + lib, "-lzp_hip", "-Wl,-rpath," + lib], check=True)
-    for m in args.modes.split(","):
-        for t in args.threads.split(","):
-            r = subprocess.run([exe, t, str(args.calls), m], input=frames, capture_output=True,
+    runs = [(m, t, lf) for m in args.modes.split(",") for t in args.threads.split(",")
+            for lf in (args.lives.split(",") if m != "0" else ["0"])]
+    for m, t, lf in runs:
+        if True:
+            r = subprocess.run([exe, t, str(args.calls), m, lf], input=frames, capture_output=True,
                                text=True, timeout=300)
             print(r.stdout.strip() or r.stderr[-2000:], flush=True)
             if r.returncode:
@@ -54,16 +57,20 @@ def py_threads(zp, frames, threads, calls):
     for f in frames[:64]:                                   # warm the pool's servers
         P.parse(f)
     lat = [[] for _ in range(threads)]
+    go = threading.Barrier(threads + 1)
 
     def run(t):
+        P.parse(frames[t])                                  # this thread's pool context
+        go.wait()
         for k in range(calls):
             t0 = time.perf_counter()
             P.parse(frames[(k * 7 + t) % len(frames)])
             lat[t].append(time.perf_counter() - t0)
     ths = [threading.Thread(target=run, args=(t,)) for t in range(threads)]
-    t0 = time.perf_counter()
     for th in ths:
         th.start()
+    go.wait()
+    t0 = time.perf_counter()
     for th in ths:
         th.join()
     dt = time.perf_counter() - t0

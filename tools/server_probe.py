@@ -77,7 +77,10 @@ def main():
             time.sleep(0.05)
         stop.set()
         th.join()
+        st = np.zeros(3, np.uint64)
+        lib.zp__one_stats(ctx, st.ctypes.data)
         print(json.dumps({"probe": "traffic_sync", "life_us": life, "calls": n[0],
+                          "launches_rotations_relaunches": [int(x) for x in st],
                           "wait_ms": [round(1e3 * x, 3) for x in w]}), flush=True)
     lib.zp_ctx_destroy(ctx)
 

@@ -12,6 +12,7 @@ HIP_LIB = os.path.join(HERE, "libzp_hip.so")
 HOST_LIB = os.path.join(HERE, "libzp_host.so")
 
 _hip = None
+_pyhip = None
 _host = None
 
 c_u8p = ctypes.c_void_p
@@ -45,6 +46,7 @@ def hip():
         _sig(lib, "zp_parse_one_config", i32, [vp, u32])
         _sig(lib, "zp_device_current", i32, [])
         _sig(lib, "zp__one_test_hooks", i32, [vp, u32, u64, u32])   # test hook
+        _sig(lib, "zp__one_stats", i32, [vp, vp])                     # test hook
         _sig(lib, "zp_col_width", i32, [i32])
         _sig(lib, "zp_build_err_str", ctypes.c_char_p, [i32])
         _sig(lib, "zp_build_batch_device", i32, [vp, vp, vp, u64, vp, vp, vp, vp, vp])
@@ -52,6 +54,7 @@ def hip():
         _sig(lib, "zp_parse_batch_columns_device", i32, [vp, vp, vp, u64, vp, vp, vp, vp])
         _sig(lib, "zp_stats_device", i32, [vp, u64, vp, vp])
         _sig(lib, "zp_probe_read_device", i32, [vp, u64, vp, vp])
+        _sig(lib, "zp_probe_tiles_device", i32, [vp, u64, u64, vp, vp, vp])
         _sig(lib, "zp_gen_lengths_device", i32, [i32, u64, u64, u64, vp, vp])
         _sig(lib, "zp_gen_frames_device", i32, [i32, u64, u64, u64, vp, vp, vp, vp])
         _sig(lib, "zp_reader_new", i32, [i32, vp, u64, vp])
@@ -61,6 +64,24 @@ def hip():
         _sig(lib, "zp_rec_decode", i32, [vp, vp, u64, vp, vp])
         _hip = lib
     return _hip
+
+
+def pyhip():
+    """libzp_hip.so through ctypes.PyDLL: calls that keep the GIL. For
+    zp_parse_one on a frame the resident server answers (~4.5 us), holding
+    the GIL is cheaper than handing it over: a hand-off costs the waiting
+    thread's wake-up (several us), and with several Python threads parsing
+    at once the hand-offs convoy (8 threads: 47k calls/s and an 81 us p50
+    against 118k / 8.6 us on one thread, profiles/r06_parse_one_latency.log)."""
+    global _pyhip
+    if _pyhip is None:
+        hip()
+        lib = ctypes.PyDLL(HIP_LIB)
+        _sig(lib, "zp_device_current", ctypes.c_int, [])
+        vp, u64 = ctypes.c_void_p, ctypes.c_uint64
+        _sig(lib, "zp_parse_one", ctypes.c_int, [vp, vp, u64, vp, vp])
+        _pyhip = lib
+    return _pyhip
 
 
 def host():

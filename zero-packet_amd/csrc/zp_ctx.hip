@@ -56,17 +56,11 @@ struct zp_ctx {
     uint8_t* one_h;
     uint8_t* one_d;
     bool one_failed;              // the mapped block could not be allocated: batch path
-    // ... and its resident server wave (zp_one_server_kernel, zp_parse.hip)
-    uint32_t one_idle_us;         // server idle timeout; 0: one batch launch per call
-    uint32_t one_life_us;         // server residency bound (ONE_LIFE_US_DEFAULT)
-    uint64_t one_clock_khz;       // the device's constant clock (s_memrealtime)
-    uint32_t one_seq;             // last request answered (or retired by a stop)
-    hipStream_t srv;              // the server's stream
-    bool srv_live;                // a server was launched and may still run
-    int64_t srv_seen_ns;          // host clock when the server last showed activity
-    int64_t srv_born_ns;          // host clock when the newest server was launched
+    // ... served by a wave of the device's shared server (SharedServer below)
+    uint32_t one_idle_us;         // 0: one batch launch per call; > 0: the shared server
+    uint32_t one_seq;             // last request answered (or retired by a give-up)
+    int slot;                     // this context's slot in the device's server (-1: none)
     int64_t one_giveup_ns;        // no answer for this long: the request fails (-2)
-    uint32_t one_stall_us;        // test hook: a stall kernel before each server launch
 };
 
 // zp_parse_one's block: the frame at ONE_FRAME, the doorbell and the batch
@@ -83,19 +77,17 @@ struct zp_ctx {
 #define ONE_EXT 96       // zp_ext_offsets[2]
 #define ONE_FRAME 128
 #define ONE_MAX (64u << 10)
-#define ONE_STOP 0xFFFFFFFFu          // doorbell length: the server leaves
-#define ONE_IDLE_US_DEFAULT 5000u     // server idle timeout
-#define ONE_LIFE_US_DEFAULT 1000u     // a server leaves after this long resident, busy or not
-#define ONE_MARGIN_NS 500000          // host/device clock slack when judging the server alive
-#define ONE_LIFE_MARGIN_NS 100000     // ... and before its life ends (the host relaunches it)
+#define ONE_IDLE_US_DEFAULT 5000u     // zp_parse_one_config's default (> 0: the server)
+#define ONE_LIFE_US_DEFAULT 1000u     // a server kernel leaves after this long resident
+#define ONE_LIFE_MARGIN_NS 100000     // the host replaces it this long before its life ends
 #define ONE_GIVEUP_NS 10000000000ll   // 10 s without an answer: the request fails
 #define ONE_TAG_KEY 0x9E3779B9u       // ZP_ONE_TAG (zp_parse.hip)
 
 static_assert(ONE_FRAME + ONE_MAX + 64 == 128u + (64u << 10) + 64u,
               "the server's buffer range (ZP_SYS_BYTES, zp_stream.h) is the mapped block");
 
-extern "C" int zp__one_server_launch(uint8_t* blk_d, uint64_t idle_ticks, uint64_t life_ticks,
-                                     void* stream);
+extern "C" int zp__one_server_launch(const uint8_t* ctl_d, uint32_t nslots, uint64_t life_ticks,
+                                     uint32_t gen, void* stream);
 extern "C" int zp__one_stall_launch(uint64_t ticks, void* stream);
 
 static int64_t mono_ns() {
@@ -128,20 +120,192 @@ static hipError_t grow(T** p, uint64_t* cap, uint64_t need) {
         }                                                                          \
     } while (0)
 
-// Stops the context's zp_parse_one servers (the running one and any queued
-// behind it) and waits for them. Every one of them leaves without answering
-// a request: a server starts from the acknowledgement word, and the stop
-// doorbell is newer. The stop's seq then becomes the acknowledgement, so the
-// next launch starts from it.
+// --------------------------------------------------------------------------
+// The device's shared zp_parse_one server. One kernel per device (process
+// wide) serves every context of that device: wave w of its grid polls slot
+// w's doorbell (the context's mapped block, registered in a table in the
+// control block) and answers its requests. One kernel rather than one per
+// context: a resident kernel holds its hardware queue, and the process has
+// few (GPU_MAX_HW_QUEUES, 4 here), so per-context servers past the fourth
+// waited behind the others (profiles/r06_parse_one_latency.log). The kernel
+// leaves after `life` (1 ms) whatever the traffic; shortly before, the next
+// caller queues a new generation behind it and writes the retire word, so
+// the old one leaves at its next poll and the new one starts from each
+// slot's acknowledgement word (nothing is answered twice). A device-wide
+// synchronisation therefore waits for about one life at most.
+// --------------------------------------------------------------------------
+#define SRV_SLOTS 64                  // contexts per device with a server slot
+#define CTL_RETIRE 0                  // uint32_t: kernels of generation <= this leave
+#define CTL_TABLE 64                  // uint64_t[SRV_SLOTS]: each slot's block (device VA, 0: none)
+#define CTL_BYTES (CTL_TABLE + 8 * SRV_SLOTS)
+#define SRV_DEVICES 64
+
+struct SharedServer {
+    pthread_mutex_t m;            // launches, rotations, slots (not the request path)
+    bool ready, failed;
+    hipStream_t stream;
+    uint8_t* ctl_h;               // mapped, coherent control block
+    uint8_t* ctl_d;
+    uint64_t clock_khz;           // the device's constant clock (s_memrealtime)
+    uint64_t used;                // slot bitmap
+    uint32_t nslots;              // slots in use span [0, nslots)
+    uint32_t gen;                 // newest generation launched
+    int64_t born_ns;              // atomic: host clock of the newest launch (0: none runs)
+    uint32_t life_us;             // atomic (test hook zp__one_test_hooks)
+    uint32_t stall_us;            // test hook: a stall kernel before each launch
+    uint64_t launches, rotations, relaunches;
+};
+static SharedServer g_srv[SRV_DEVICES];
+static pthread_mutex_t g_srv_init = PTHREAD_MUTEX_INITIALIZER;
+static bool g_srv_mutex[SRV_DEVICES];
+
+// The device's server (its stream and control block on first use; the
+// caller has set the device). NULL: none (the batch path serves).
+static SharedServer* srv_get(int device) {
+    if (device < 0 || device >= SRV_DEVICES) return NULL;
+    SharedServer* S = &g_srv[device];
+    pthread_mutex_lock(&g_srv_init);
+    if (!g_srv_mutex[device]) {
+        pthread_mutex_init(&S->m, NULL);
+        g_srv_mutex[device] = true;
+    }
+    pthread_mutex_unlock(&g_srv_init);
+    pthread_mutex_lock(&S->m);
+    if (!S->ready && !S->failed) {
+        int khz = 0;
+        hipError_t e = hipStreamCreateWithFlags(&S->stream, hipStreamNonBlocking);
+        if (e == hipSuccess)
+            e = hipHostMalloc((void**)&S->ctl_h, CTL_BYTES, hipHostMallocMapped | hipHostMallocCoherent);
+        if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&S->ctl_d, S->ctl_h, 0);
+        if (e == hipSuccess) e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device);
+        if (e == hipSuccess) {
+            memset(S->ctl_h, 0, CTL_BYTES);
+            S->clock_khz = (uint64_t)(khz > 0 ? khz : 100000);
+            __atomic_store_n(&S->life_us, ONE_LIFE_US_DEFAULT, __ATOMIC_RELAXED);
+            S->ready = true;
+        } else {
+            (void)hipGetLastError();
+            S->failed = true;                       // the batch path serves (not retried)
+        }
+    }
+    const bool ok = S->ready;
+    pthread_mutex_unlock(&S->m);
+    return ok ? S : NULL;
+}
+
+// True when a server kernel surely still runs: launched less than its life
+// ago (host clock; the device counts from a later instant).
+static bool srv_sure(SharedServer* S, int64_t now) {
+    const int64_t born = __atomic_load_n(&S->born_ns, __ATOMIC_ACQUIRE);
+    const int64_t life = (int64_t)__atomic_load_n(&S->life_us, __ATOMIC_RELAXED) * 1000;
+    return born != 0 && now - born < life - ONE_LIFE_MARGIN_NS;
+}
+
+// Launches generation gen + 1 behind whatever runs on the server stream
+// (S->m held).
+static int srv_launch_locked(SharedServer* S) {
+    const uint64_t life = (uint64_t)__atomic_load_n(&S->life_us, __ATOMIC_RELAXED) * S->clock_khz / 1000u;
+    if (S->stall_us) {
+        const int rc = zp__one_stall_launch((uint64_t)S->stall_us * S->clock_khz / 1000u, S->stream);
+        if (rc) return rc;
+    }
+    const int rc = zp__one_server_launch(S->ctl_d, S->nslots, life, S->gen + 1u, S->stream);
+    if (rc) return rc;
+    ++S->gen;
+    ++S->launches;
+    __atomic_store_n(&S->born_ns, mono_ns(), __ATOMIC_RELEASE);
+    return 0;
+}
+
+// Replaces the running kernel (if any) by a new generation: the new one is
+// queued, then the old one retired (S->m held).
+static int srv_rotate_locked(SharedServer* S) {
+    const bool live = __atomic_load_n(&S->born_ns, __ATOMIC_ACQUIRE) != 0;
+    const int rc = srv_launch_locked(S);
+    if (rc) return rc;
+    if (live) {
+        __atomic_store_n((uint32_t*)(S->ctl_h + CTL_RETIRE), S->gen - 1u, __ATOMIC_RELEASE);
+        ++S->rotations;
+    }
+    return 0;
+}
+
+// A server runs that includes every registered slot, or is launched (the
+// caller has set the device). Called when srv_sure said no.
+static int srv_ensure(SharedServer* S) {
+    pthread_mutex_lock(&S->m);
+    int rc = 0;
+    if (!srv_sure(S, mono_ns())) {                    // another thread may have done it
+        if (__atomic_load_n(&S->born_ns, __ATOMIC_ACQUIRE) != 0) {
+            const hipError_t q = hipStreamQuery(S->stream);
+            if (q == hipSuccess) {
+                __atomic_store_n(&S->born_ns, (int64_t)0, __ATOMIC_RELEASE);
+            } else if (q != hipErrorNotReady) {
+                snprintf(g_ctx_error, ERRBUF_LEN, "zp_parse_one server: %s", hipGetErrorString(q));
+                __atomic_store_n(&S->born_ns, (int64_t)0, __ATOMIC_RELEASE);
+                rc = -2;
+            }
+        }
+        if (!rc) rc = srv_rotate_locked(S);          // a launch when none runs
+    }
+    pthread_mutex_unlock(&S->m);
+    return rc;
+}
+
+// Retires every generation and waits for the server stream (S->m held).
+static void srv_stop_locked(SharedServer* S) {
+    if (__atomic_load_n(&S->born_ns, __ATOMIC_ACQUIRE) == 0 && hipStreamQuery(S->stream) == hipSuccess)
+        return;
+    __atomic_store_n((uint32_t*)(S->ctl_h + CTL_RETIRE), S->gen, __ATOMIC_RELEASE);
+    (void)hipStreamSynchronize(S->stream);
+    __atomic_store_n(&S->born_ns, (int64_t)0, __ATOMIC_RELEASE);
+}
+
+// The context's slot (registered on first use; a running kernel is replaced
+// so that the new slot is served). False: no free slot (the launch mode
+// serves this context).
+static bool srv_register(SharedServer* S, zp_ctx* c) {
+    if (c->slot >= 0) return true;
+    pthread_mutex_lock(&S->m);
+    int k = 0;
+    while (k < SRV_SLOTS && (S->used >> k) & 1u) ++k;
+    if (k < SRV_SLOTS) {
+        S->used |= 1ull << k;
+        if ((uint32_t)k + 1u > S->nslots) S->nslots = (uint32_t)k + 1u;
+        __atomic_store_n((uint64_t*)(S->ctl_h + CTL_TABLE + 8 * k), (uint64_t)(uintptr_t)c->one_d,
+                         __ATOMIC_RELEASE);
+        c->slot = k;
+        if (__atomic_load_n(&S->born_ns, __ATOMIC_ACQUIRE) != 0 &&
+            hipStreamQuery(S->stream) == hipErrorNotReady)
+            (void)srv_rotate_locked(S);
+        else
+            __atomic_store_n(&S->born_ns, (int64_t)0, __ATOMIC_RELEASE);
+    }
+    pthread_mutex_unlock(&S->m);
+    return c->slot >= 0;
+}
+
+// Stops the device's server (every context's next call relaunches it).
 static void one_server_stop(zp_ctx* c) {
-    if (!c->srv_live) return;
-    const uint32_t stop = c->one_seq + 1u;
-    __atomic_store_n((uint64_t*)(c->one_h + ONE_BELL), ((uint64_t)stop << 32) | ONE_STOP,
-                     __ATOMIC_RELEASE);
-    (void)hipStreamSynchronize(c->srv);
-    c->one_seq = stop;
-    __atomic_store_n((uint32_t*)(c->one_h + ONE_ACK), stop, __ATOMIC_RELEASE);
-    c->srv_live = false;
+    if (c->slot < 0) return;
+    SharedServer* S = &g_srv[c->device];
+    pthread_mutex_lock(&S->m);
+    srv_stop_locked(S);
+    pthread_mutex_unlock(&S->m);
+}
+
+// Takes the context's slot out of the table; the server is stopped first,
+// so no wave reads the block afterwards.
+static void srv_unregister(zp_ctx* c) {
+    if (c->slot < 0) return;
+    SharedServer* S = &g_srv[c->device];
+    pthread_mutex_lock(&S->m);
+    srv_stop_locked(S);
+    __atomic_store_n((uint64_t*)(S->ctl_h + CTL_TABLE + 8 * c->slot), (uint64_t)0, __ATOMIC_RELEASE);
+    S->used &= ~(1ull << c->slot);
+    while (S->nslots && !((S->used >> (S->nslots - 1)) & 1u)) --S->nslots;
+    c->slot = -1;
+    pthread_mutex_unlock(&S->m);
 }
 
 extern "C" void zp_ctx_destroy(zp_ctx* c) {
@@ -149,8 +313,7 @@ extern "C" void zp_ctx_destroy(zp_ctx* c) {
     int prev = 0;
     (void)hipGetDevice(&prev);
     (void)hipSetDevice(c->device);
-    one_server_stop(c);
-    if (c->srv) (void)hipStreamDestroy(c->srv);
+    srv_unregister(c);
     for (int k = 0; k < SLOTS; ++k) {
         if (c->s[k]) (void)hipStreamSynchronize(c->s[k]);
         (void)hipFree(c->d_arena[k]); (void)hipFree(c->d_offs[k]); (void)hipFree(c->d_lens[k]);
@@ -175,8 +338,8 @@ extern "C" zp_ctx* zp_ctx_create(int device, uint64_t chunk_bytes) {
     c->device = device;
     c->chunk_bytes = chunk_bytes;
     c->one_idle_us = ONE_IDLE_US_DEFAULT;
-    c->one_life_us = ONE_LIFE_US_DEFAULT;
     c->one_giveup_ns = ONE_GIVEUP_NS;
+    c->slot = -1;
     c->chunk_pkts = chunk_bytes / 64 + 1;
     (void)hipGetDevice(&prev);
     TRY(hipSetDevice(device));
@@ -193,12 +356,6 @@ extern "C" zp_ctx* zp_ctx_create(int device, uint64_t chunk_bytes) {
         TRY(hipHostMalloc(&c->h_lens[k], c->chunk_pkts * sizeof(uint32_t), hipHostMallocDefault));
         TRY(hipHostMalloc(&c->h_rec[k], c->chunk_pkts * sizeof(zp_record), hipHostMallocDefault));
         TRY(hipHostMalloc(&c->h_ext[k], 2 * c->chunk_pkts * sizeof(zp_ext_offsets), hipHostMallocDefault));
-    }
-    TRY(hipStreamCreateWithFlags(&c->srv, hipStreamNonBlocking));
-    {
-        int khz = 0;
-        TRY(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device));
-        c->one_clock_khz = (uint64_t)(khz > 0 ? khz : 100000);
     }
     (void)hipSetDevice(prev);
     return c;
@@ -355,69 +512,24 @@ static bool one_block(zp_ctx* c) {
     return c->one_h != NULL;
 }
 
-// Launches a server behind whatever runs on the server stream (a server
-// about to reach its life waits for nothing more than that).
-static int one_server_launch(zp_ctx* c, int64_t now) {
-    const uint64_t idle = (uint64_t)c->one_idle_us * c->one_clock_khz / 1000u;
-    const uint64_t life = (uint64_t)c->one_life_us * c->one_clock_khz / 1000u;
-    if (c->one_stall_us) {
-        const int rc = zp__one_stall_launch((uint64_t)c->one_stall_us * c->one_clock_khz / 1000u,
-                                            c->srv);
+// One request through the device's server: doorbell, then spin on the
+// acknowledgement. The answer is the 16-B {record, ack, tag} read as one
+// load; an ack whose tag does not match the record read with it is waited
+// out (a host-link write seen in pieces). On giving up, the request is
+// retired (the acknowledgement word takes its seq) only after the server has
+// been stopped, so a late wave never answers it from a frame being
+// rewritten. `sure`: a kernel surely runs (else the caller has set the
+// device and one is ensured first).
+static int one_via_server(zp_ctx* c, SharedServer* S, uint32_t len, zp_record* out, bool sure) {
+    if (!sure) {
+        const int rc = srv_ensure(S);
         if (rc) return rc;
-    }
-    const int rc = zp__one_server_launch(c->one_d, idle, life, c->srv);
-    if (rc) return rc;
-    c->srv_live = true;
-    c->srv_seen_ns = now;
-    c->srv_born_ns = now;
-    return 0;
-}
-
-// True when the server surely still runs: it answered less than its idle
-// timeout ago and it was launched less than its life ago (host clock; the
-// device counts both from later instants, so the estimate is conservative).
-static bool one_server_sure(const zp_ctx* c, int64_t now) {
-    return c->srv_live && now - c->srv_seen_ns < (int64_t)c->one_idle_us * 1000 - ONE_MARGIN_NS &&
-           now - c->srv_born_ns < (int64_t)c->one_life_us * 1000 - ONE_LIFE_MARGIN_NS;
-}
-
-// One request through the resident server: doorbell, then spin on the
-// acknowledgement. When the server may have left (or is about to, at its
-// life), a new one is queued behind it on its stream first; it starts from
-// the acknowledgement word, so nothing is answered twice. The answer is the
-// 16-B {record, ack, tag} read as one load; an ack whose tag does not match
-// the record read with it is waited out (a host-link write seen in pieces).
-// On giving up, the request is retired and the servers stopped before the
-// block is written again (a late server must not answer it from a frame
-// being rewritten).
-static int one_via_server(zp_ctx* c, uint32_t len, zp_record* out, bool sure, int64_t now) {
-    if (!sure) {                                             // the caller set the device
-        // Launch when no server runs, or queue the next one behind the
-        // running one when its life is nearly over; a running one whose idle
-        // timeout may have passed answers, or, if it just left, the check
-        // below relaunches (rare: the window is the host link's latency).
-        bool launch = !c->srv_live;
-        if (!launch) {
-            const hipError_t q = hipStreamQuery(c->srv);
-            if (q == hipSuccess) launch = true;
-            else if (q != hipErrorNotReady) {
-                snprintf(g_ctx_error, ERRBUF_LEN, "zp_parse_one server: %s", hipGetErrorString(q));
-                c->srv_live = false;
-                return -2;
-            } else {
-                launch = now - c->srv_born_ns >= (int64_t)c->one_life_us * 1000 - ONE_LIFE_MARGIN_NS;
-            }
-        }
-        if (launch) {
-            const int rc = one_server_launch(c, now);
-            if (rc) return rc;
-        }
     }
     const uint32_t seq = c->one_seq + 1u;
     const volatile __m128i* ans = (const volatile __m128i*)(c->one_h + ONE_REC);
     __atomic_store_n((uint64_t*)(c->one_h + ONE_BELL), ((uint64_t)seq << 32) | len,
                      __ATOMIC_RELEASE);
-    const int64_t t0 = now;
+    const int64_t t0 = mono_ns();
     int64_t next_check = t0 + 200000;                        // 200 us
     uint32_t w[4];
     for (uint32_t spin = 1;; ++spin) {
@@ -426,29 +538,38 @@ static int one_via_server(zp_ctx* c, uint32_t len, zp_record* out, bool sure, in
         if (w[2] == seq && w[3] == (w[0] ^ w[1] ^ seq ^ ONE_TAG_KEY)) break;
         _mm_pause();
         if ((spin & 1023u) == 0) {
-            now = mono_ns();
+            const int64_t now = mono_ns();
             if (now < next_check) continue;
-            // The servers may all have left before the doorbell (their
-            // timeouts): then the stream is done and the request still open.
-            const hipError_t q = hipStreamQuery(c->srv);
+            // The kernel may have left before the doorbell (its life, or
+            // quiesced by another thread): then its stream is done and the
+            // request still open.
+            const hipError_t q = hipStreamQuery(S->stream);
             if (q == hipSuccess) {
                 int prev = 0;
                 (void)hipGetDevice(&prev);
                 (void)hipSetDevice(c->device);
-                const int rc = one_server_launch(c, now);
+                pthread_mutex_lock(&S->m);
+                int rc = 0;
+                if (hipStreamQuery(S->stream) == hipSuccess) {
+                    __atomic_store_n(&S->born_ns, (int64_t)0, __ATOMIC_RELEASE);
+                    rc = srv_launch_locked(S);
+                    ++S->relaunches;
+                }
+                pthread_mutex_unlock(&S->m);
                 (void)hipSetDevice(prev);
                 if (rc) return rc;
             } else if (q != hipErrorNotReady) {
                 snprintf(g_ctx_error, ERRBUF_LEN, "zp_parse_one server: %s", hipGetErrorString(q));
-                c->srv_live = false;
+                __atomic_store_n(&S->born_ns, (int64_t)0, __ATOMIC_RELEASE);
                 return -2;
             }
             if (now - t0 > c->one_giveup_ns) {
                 int prev = 0;
                 (void)hipGetDevice(&prev);
                 (void)hipSetDevice(c->device);
+                one_server_stop(c);                         // no wave runs after this
                 c->one_seq = seq;                           // retired: never answered later
-                one_server_stop(c);
+                __atomic_store_n((uint32_t*)(c->one_h + ONE_ACK), seq, __ATOMIC_RELEASE);
                 (void)hipSetDevice(prev);
                 snprintf(g_ctx_error, ERRBUF_LEN, "zp_parse_one: no answer from the server");
                 return -2;
@@ -457,7 +578,6 @@ static int one_via_server(zp_ctx* c, uint32_t len, zp_record* out, bool sure, in
         }
     }
     c->one_seq = seq;
-    c->srv_seen_ns = mono_ns();
     memcpy(out, w, sizeof(zp_record));
     return 0;
 }
@@ -473,12 +593,12 @@ extern "C" int zp_parse_one(zp_ctx* c, const uint8_t* frame, uint64_t len,
     if (!c || !record || len > 0xFFFFFFFFull || (!frame && len)) return -1;
     int rc;
     uint8_t* h = c->one_h;
-    const int64_t now = mono_ns();
-    if (h && len <= ONE_MAX && c->one_idle_us && one_server_sure(c, now)) {
-        // The fast path: the server surely runs, so no HIP call at all:
+    SharedServer* S = c->slot >= 0 ? &g_srv[c->device] : NULL;
+    if (S && len <= ONE_MAX && c->one_idle_us && srv_sure(S, mono_ns())) {
+        // The fast path: a server kernel surely runs, so no HIP call at all:
         // copy, doorbell, spin.
         if (len) memcpy(h + ONE_FRAME, frame, len);
-        rc = one_via_server(c, (uint32_t)len, record, true, now);
+        rc = one_via_server(c, S, (uint32_t)len, record, true);
     } else {
         int prev = 0;
         (void)hipGetDevice(&prev);
@@ -494,8 +614,12 @@ extern "C" int zp_parse_one(zp_ctx* c, const uint8_t* frame, uint64_t len,
         }
         h = c->one_h;
         if (len) memcpy(h + ONE_FRAME, frame, len);
-        if (c->one_idle_us) {
-            rc = one_via_server(c, (uint32_t)len, record, false, now);
+        if (c->one_idle_us && !S) {
+            S = srv_get(c->device);
+            if (S && !srv_register(S, c)) S = NULL;
+        }
+        if (c->one_idle_us && S) {
+            rc = one_via_server(c, S, (uint32_t)len, record, false);
         } else {
             const uint64_t at = ONE_FRAME;
             const uint32_t l = (uint32_t)len;
@@ -530,9 +654,10 @@ extern "C" int zp_parse_one(zp_ctx* c, const uint8_t* frame, uint64_t len,
 
 
 // zp_parse_one's mode: idle_us = 0 launches the batch kernel per call;
-// otherwise a resident server wave answers and leaves after idle_us without
-// a request. Stops a running server either way (so this also quiesces the
-// context before a device-wide synchronisation).
+// otherwise the device's shared server answers (it leaves after its 1 ms
+// life, so the value is not a timeout any more). Stops the device's server
+// either way (so this also quiesces it before a device-wide synchronisation;
+// every context's next call relaunches it).
 extern "C" int zp_parse_one_config(zp_ctx* c, uint32_t idle_us) {
     if (!c) return -1;
     int prev = 0;
@@ -554,17 +679,38 @@ extern "C" int zp_device_current(void) {
     return d;
 }
 
-// Test hook (tests/test_gpu_parity.py, not in zero_packet.h): the server's
-// life and the give-up time in us (0: keep), and a stall of stall_us queued
-// in front of every server launch (0: none). Stops a running server.
+// Test hook: the device server's counters (launches, rotations, relaunches
+// by the answer wait's stream check).
+extern "C" int zp__one_stats(const zp_ctx* c, uint64_t* out) {
+    if (!c || !out || c->device < 0 || c->device >= SRV_DEVICES) return -1;
+    const SharedServer* S = &g_srv[c->device];
+    out[0] = S->launches;
+    out[1] = S->rotations;
+    out[2] = S->relaunches;
+    return 0;
+}
+
+// Test hook (tests/test_gpu_parity.py, not in zero_packet.h): the device
+// server's life (us, 0: keep) and a stall of stall_us queued in front of
+// each of its launches (0: none), and this context's give-up time (us, 0:
+// keep). Stops the device's server.
 extern "C" int zp__one_test_hooks(zp_ctx* c, uint32_t life_us, uint64_t giveup_us,
                                   uint32_t stall_us) {
     if (!c) return -1;
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    if (hipSetDevice(c->device) != hipSuccess) return -2;
+    SharedServer* S = srv_get(c->device);
+    (void)hipSetDevice(prev);
+    if (!S) return -2;
     const int rc = zp_parse_one_config(c, c->one_idle_us);
     if (rc) return rc;
-    if (life_us) c->one_life_us = life_us;
+    pthread_mutex_lock(&S->m);
+    srv_stop_locked(S);
+    if (life_us) __atomic_store_n(&S->life_us, life_us, __ATOMIC_RELAXED);
+    S->stall_us = stall_us;
+    pthread_mutex_unlock(&S->m);
     if (giveup_us) c->one_giveup_ns = (int64_t)giveup_us * 1000;
-    c->one_stall_us = stall_us;
     return 0;
 }
 

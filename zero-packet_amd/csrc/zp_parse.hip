@@ -1089,20 +1089,20 @@ extern "C" int zp_parse_batch_columns_device(const uint8_t* arena, const uint64_
 // zp_parse_one's resident server (zp_ctx.hip). PacketParser::parse for one
 // frame (parser.rs:53) costs a kernel launch and its completion signal when
 // each call launches the batch kernel (17.5 us). Instead one
-// wave per context stays resident and polls a doorbell in the context's
-// mapped host block: the host writes the frame, then the 64-bit doorbell
-// (sequence << 32 | length); the wave sees it, parses the frame in place as
-// a one-frame tile (parse_tile, the batch kernel's own code), writes the
-// chains back into the block, and then the record, the sequence number and a
-// tag in one 16-B store. The wave leaves when it has seen no request for
-// `idle` ticks of the 100 MHz constant clock (s_memrealtime), when it has
-// been resident for `life` ticks (1 ms by default, whatever the traffic), or
-// when the doorbell carries ZP_ONE_STOP, so it never spins past use and a
-// device-wide synchronisation never waits longer than its life; the host
-// relaunches it (zp_ctx.hip: the host knows from its own clock when the wave
-// may leave and queues the next one behind it on the same stream).
-// Memory order: the host block is fine-grained (coherent) host memory. The
-// doorbell, the acknowledgement read at start and the frame bytes (stream
+// kernel per device stays resident, one wave per context slot, each polling
+// a doorbell in its context's mapped host block: the host writes the frame,
+// then the 64-bit doorbell (sequence << 32 | length); the wave sees it,
+// parses the frame in place as a one-frame tile (the batch kernel's own
+// tile_finish), writes the chains back into the block, and then the record,
+// the sequence number and a tag in one 16-B store. The kernel leaves when it
+// has been resident for `life` ticks of the 100 MHz constant clock
+// (s_memrealtime; 1 ms by default, whatever the traffic) or when the retire
+// word of the control block reaches its generation (the host queued the
+// next generation behind it, or stops the server), so it never spins past
+// use and a device-wide synchronisation waits for about one life at most.
+// Memory order: the blocks are fine-grained (coherent) host memory. The
+// doorbell, the retire word, the slot table and acknowledgement read at
+// start and the frame bytes (stream
 // and fallback loads) are read with system-scope loads (sc0 sc1, past both
 // caches), so a frame the host rewrote since the last request is never
 // served from a cache and no cache-wide invalidate is needed; the record and
@@ -1115,8 +1115,9 @@ extern "C" int zp_parse_batch_columns_device(const uint8_t* arena, const uint64_
                              // seq of the last finished request
 #define ZP_ONE_EXT 96        // zp_ext_offsets[2] (server writes)
 #define ZP_ONE_FRAME 128     // the frame (host writes)
-#define ZP_ONE_STOP 0xFFFFFFFFu   // doorbell length: leave now
 #define ZP_ONE_TAG 0x9E3779B9u    // answer tag: rec.x ^ rec.y ^ seq ^ ZP_ONE_TAG (zp_ctx.hip)
+#define ZP_CTL_RETIRE 0      // control block (zp_ctx.hip SharedServer): uint32_t retire word
+#define ZP_CTL_TABLE 64      // ... and uint64_t[64]: each slot's block
 
 // The one frame of a zp_parse_one request, streamed by the server wave: its
 // chunks [A & ~15, E) are contiguous, so lane l of item i simply loads chunk
@@ -1170,45 +1171,55 @@ __device__ __forceinline__ void one_frame_tile(uint32_t len, uintptr_t ga, int l
 }
 
 __global__ void __launch_bounds__(64)
-zp_one_server_kernel(uint8_t* blk, uint64_t idle, uint64_t life) {
+zp_one_server_kernel(const uint8_t* ctl, uint64_t life, uint32_t gen) {
     __shared__ WaveLds lds;
     const int lane = threadIdx.x & 63;
-    // The last answered request is the acknowledgement word in the block (the
-    // previous wave's, or the host's after a stop): a wave queued behind
-    // another never answers a request twice, and answers one rung while it
-    // waited for the stream.
+    // This wave's slot: the block of one context (the table in the control
+    // block, zp_ctx.hip SharedServer); an empty slot has nothing to serve.
+    uint64_t b = 0;
+    if (lane == 0)
+        b = __hip_atomic_load((const uint64_t*)(ctl + ZP_CTL_TABLE) + blockIdx.x, __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_SYSTEM);
+    uint8_t* blk = (uint8_t*)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(b >> 32), 0) << 32) |
+                              (uint32_t)__builtin_amdgcn_readlane((uint32_t)b, 0));
+    if (!blk) return;
+    // The last answered request is the slot's acknowledgement word (the
+    // previous generation's, or the host's after a give-up): a wave never
+    // answers a request twice, and answers one rung while it waited for the
+    // stream.
     uint32_t seq = 0;
     if (lane == 0)
         seq = __hip_atomic_load((const uint32_t*)(blk + ZP_ONE_ACK), __ATOMIC_RELAXED,
                                 __HIP_MEMORY_SCOPE_SYSTEM);
     seq = (uint32_t)__builtin_amdgcn_readlane(seq, 0);
-    // One system-scope poll of the doorbell in flight, from lane 0 only
-    // (loads of one address from several lanes are not merged and cost
-    // ~0.1 us each). Measured and not kept (profiles/r05_parse_one_server_
-    // iterations.log): four polling waves (7.2 us per call: they slow the
-    // working wave's host accesses), and several polls in flight from this
-    // wave (the compiler waits for all of them at the rotation's head).
-    // The wave leaves after `idle` ticks without a request and, whatever the
-    // traffic, once it has been resident for `life` ticks: a device-wide
-    // synchronisation issued meanwhile (hipDeviceSynchronize,
-    // torch.cuda.synchronize, hipFree) waits at most that long. The host
-    // relaunches it behind the old one on the same stream (zp_ctx.hip).
+    // One system-scope poll of the doorbell in flight, from lane 0 (loads of
+    // one address from several lanes are not merged and cost ~0.1 us each),
+    // and of the retire word from lane 1, in one load instruction. Measured
+    // and not kept (profiles/r05_parse_one_server_iterations.log): four
+    // polling waves per slot (7.2 us per call: they slow the working wave's
+    // host accesses), and several polls in flight from this wave (the
+    // compiler waits for all of them at the rotation's head).
+    // The kernel leaves once it has been resident for `life` ticks, or at
+    // once when the retire word reaches its generation (the host queued the
+    // next one behind it or stops the server): a device-wide synchronisation
+    // issued meanwhile (hipDeviceSynchronize, torch.cuda.synchronize,
+    // hipFree) waits about that long at most.
     const uint64_t born = __builtin_amdgcn_s_memrealtime();
-    uint64_t last = born;
     for (;;) {
         uint64_t bell = 0;
-        if (lane == 0)
-            bell = __hip_atomic_load((const uint64_t*)(blk + ZP_ONE_BELL), __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_SYSTEM);
+        if (lane < 2)
+            bell = __hip_atomic_load(lane ? (const uint64_t*)(ctl + ZP_CTL_RETIRE)
+                                          : (const uint64_t*)(blk + ZP_ONE_BELL),
+                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         const uint32_t bseq = (uint32_t)__builtin_amdgcn_readlane((uint32_t)(bell >> 32), 0);
         const uint32_t blen = (uint32_t)__builtin_amdgcn_readlane((uint32_t)bell, 0);
+        const uint32_t retire = (uint32_t)__builtin_amdgcn_readlane((uint32_t)bell, 1);
+        if ((int32_t)(retire - gen) >= 0) break;             // a newer generation / a stop
         if (bseq == seq) {
-            const uint64_t now = __builtin_amdgcn_s_memrealtime();
-            if (now - last > idle || now - born > life) break;
+            if (__builtin_amdgcn_s_memrealtime() - born > life) break;
             __builtin_amdgcn_s_sleep(1);                     // ~64 clocks between polls
             continue;
         }
-        if (blen == ZP_ONE_STOP) break;
         seq = bseq;
         {                                                    // a request (wave-uniform)
             __builtin_amdgcn_s_setprio(1);
@@ -1232,18 +1243,19 @@ zp_one_server_kernel(uint8_t* blk, uint64_t idle, uint64_t life) {
                          zp_u32x4{rec.x, rec.y, bseq, rec.x ^ rec.y ^ bseq ^ ZP_ONE_TAG});
             wave_lds_fence();                                 // LDS reused by the next request
             __builtin_amdgcn_s_setprio(0);                    // polls at the base priority
-            last = __builtin_amdgcn_s_memrealtime();
-            if (last - born > life) break;
+            if (__builtin_amdgcn_s_memrealtime() - born > life) break;
         }
     }
 }
 
-extern "C" __attribute__((visibility("hidden"))) int zp__one_server_launch(uint8_t* blk_d,
-                                                                            uint64_t idle_ticks,
+extern "C" __attribute__((visibility("hidden"))) int zp__one_server_launch(const uint8_t* ctl_d,
+                                                                            uint32_t nslots,
                                                                             uint64_t life_ticks,
+                                                                            uint32_t gen,
                                                                             void* stream) {
-    hipLaunchKernelGGL(zp_one_server_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, blk_d,
-                       idle_ticks, life_ticks);
+    if (nslots == 0) return 0;
+    hipLaunchKernelGGL(zp_one_server_kernel, dim3(nslots), dim3(64), 0, (hipStream_t)stream, ctl_d,
+                       life_ticks, gen);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) { set_err("zp_one_server_kernel launch", e); return -2; }
     return 0;
