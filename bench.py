@@ -205,13 +205,14 @@ def pcie_inclusive(zp, arena, offs, lens, sample_pkts, barrier=lambda: None):
 PCIE_PATH = "pinned host -> H2D -> kernel -> D2H records, 2 streams x 256 MiB chunks"
 
 
-def placement_probe(zp, arena, n, records, kernel_ms, reps=5):
+def placement_probe(zp, arena, offs, lens, records, kernel_ms, reps=5):
     """The placement classes of the bench's own buffers, measured beside the
     parse on the launch stream (HIP events, interleaved rounds, medians):
       read      a plain grid-stride streaming read of the whole arena
                 (zp_probe_read_device): the arena's placement;
       tiles     the parse's tile pattern, reads only (zp_probe_tiles_device:
-                one wave per 64-frame slice, a parse wave's LDS);
+                one wave per 64-frame slice with a parse wave's LDS, the
+                tile's descriptors, then its slice of the arena);
       tiles_rec the same plus the 8-B record stores into the bench's records
                 buffer: tiles_rec - tiles is what the record stores cost on
                 this records placement.
@@ -221,12 +222,14 @@ def placement_probe(zp, arena, n, records, kernel_ms, reps=5):
     sink = torch.zeros(1, dtype=torch.int32, device=arena.device)
     stream = torch.cuda.current_stream(arena.device)
     nb = arena.numel() // 16 * 16
+    n = offs.numel()
     s = ctypes.c_void_p(stream.cuda_stream)
+    od, ld = offs.data_ptr(), lens.data_ptr()
     probes = {
         "read": lambda: lib.zp_probe_read_device(arena.data_ptr(), nb, sink.data_ptr(), s),
-        "tiles": lambda: lib.zp_probe_tiles_device(arena.data_ptr(), nb, n, None,
+        "tiles": lambda: lib.zp_probe_tiles_device(arena.data_ptr(), nb, n, od, ld, None,
                                                    sink.data_ptr(), s),
-        "tiles_rec": lambda: lib.zp_probe_tiles_device(arena.data_ptr(), nb, n,
+        "tiles_rec": lambda: lib.zp_probe_tiles_device(arena.data_ptr(), nb, n, od, ld,
                                                        records.data_ptr(), sink.data_ptr(), s),
     }
     for f in probes.values():
@@ -251,8 +254,9 @@ def placement_probe(zp, arena, n, records, kernel_ms, reps=5):
             "arena_va_mod_1g": arena.data_ptr() % (1 << 30),
             "records_va_mod_1g": records.data_ptr() % (1 << 30),
             "probe": "zp_probe_read_device: grid-stride nt 16-B loads, 2048 x 256 lanes; "
-                     "zp_probe_tiles_device: one wave per 64-frame slice, nt 16-B loads, "
-                     "tiles_rec + 64 nt 8-B stores per wave into the bench's records"}
+                     "zp_probe_tiles_device: one wave per 64-frame slice, its 64 descriptors, "
+                     "nt 16-B loads, tiles_rec + 64 nt 8-B stores per wave into the bench's "
+                     "records"}
 
 
 def gather_rows(row, world, rank, dev):
@@ -446,7 +450,7 @@ def main():
                      "algorithmic_bytes_per_launch": total_bytes},
     }
     coll_dev = "cpu" if shared else dev
-    out["roofline"]["placement"] = placement_probe(zp, arena, n, records, kmean)
+    out["roofline"]["placement"] = placement_probe(zp, arena, offs, lens, records, kmean)
     if not args.no_pcie:
         # every rank's host path at once: frames of all ranks / the slowest rank
         m, nb, sec, perr = pcie_inclusive(zp, arena, offs, lens, 1 << 21, barrier)

@@ -429,14 +429,15 @@ int zp_stats_device(const zp_record* records, uint64_t n, uint64_t* counts, void
 int zp_probe_read_device(const uint8_t* p, uint64_t bytes, uint32_t* sink, void* stream);
 /* Diagnostic: the parse kernel's memory traffic without its work. Over
  * ceil(n / 64) waves (one per workgroup, with a parse wave's LDS, so at its
- * occupancy) wave t streams the t-th equal slice of [p, p + bytes) and then,
- * when records != NULL, stores the 8-B words records[64 t, 64 t + 64) ∩ [0, n)
- * (their contents are junk), as the parse stores a tile's records.
- * bench.py times it with and without the stores over the bench's own arena
- * and records (roofline.placement): the read pattern follows the arena's
- * placement, the store cost the records'. Returns 0 or negative. */
-int zp_probe_tiles_device(const uint8_t* p, uint64_t bytes, uint64_t n, zp_record* records,
-                          uint32_t* sink, void* stream);
+ * occupancy) wave t loads descriptors offs / lens [64 t, 64 t + 64) ∩ [0, n)
+ * (when both are given), streams the t-th equal slice of [p, p + bytes) and
+ * then, when records != NULL, stores the 8-B words records[64 t, 64 t + 64)
+ * ∩ [0, n) (their contents are junk), as the parse does per tile. bench.py
+ * times it over the bench's own arena, descriptors and records
+ * (roofline.placement). Returns 0 or negative. */
+int zp_probe_tiles_device(const uint8_t* p, uint64_t bytes, uint64_t n, const uint64_t* offs,
+                          const uint32_t* lens, zp_record* records, uint32_t* sink,
+                          void* stream);
 
 /* ------------------------------------------------------------------------- */
 /* Host-ring ingestion pipeline. Frames start in host */

@@ -1,0 +1,88 @@
+// Record-store probe (lab tool, not product): the parse's tile pattern
+// (zp_probe_tiles_device, zp_stats.hip) with its 8-B record stores issued in
+// other ways, to see which costs less inside the read stream.
+//   mode 0  no stores
+//   1  64 lanes x 8 B nontemporal at the tile's end (the parse's way)
+//   2  the same, default cache policy
+//   3  nontemporal, before the tile's loads (the stores' time in the wave)
+//   4  32 lanes x 16 B nontemporal at the end (same bytes, half the lanes)
+//   5  nontemporal into a 2 MiB ring (L2-resident: the cost without HBM)
+//   6  nontemporal after half of the tile's loads
+//   7  nontemporal into the arena slice just read (row locality; scratch arena)
+// and per run: k consecutive tiles per wave, LDS bytes per wave (8960: the
+// parse's 18 waves per CU; 7680: 21; 4096: the VGPR bound)
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+#define G __attribute__((address_space(1)))
+
+template <int LDSB>
+__global__ void __launch_bounds__(64) rec_probe_kernel(const uint8_t* __restrict__ p, uint64_t nchunks,
+                                                       uint64_t cpt, uint64_t n,
+                                                       const uint64_t* __restrict__ offs,
+                                                       const uint32_t* __restrict__ lens,
+                                                       uint64_t* __restrict__ rec,
+                                                       uint64_t* __restrict__ ring, int mode, int k,
+                                                       uint32_t* __restrict__ sink) {
+    __shared__ uint32_t pad[LDSB / 4];
+    const uint32_t lane = threadIdx.x;
+    const G u32x4* q = (const G u32x4*)p;
+    for (int j = 0; j < k; ++j) {
+    const uint64_t t = (uint64_t)blockIdx.x * k + j;
+    if (64 * t >= n) return;
+    const uint64_t c0 = t * cpt;
+    const uint64_t c1 = (t + 1) * cpt < nchunks ? (t + 1) * cpt : nchunks;
+    const uint64_t i = 64 * t + lane < n ? 64 * t + lane : n - 1;
+    uint32_t acc = (uint32_t)offs[i] ^ lens[i];
+    const uint64_t word = ((uint64_t)lane << 32) | (uint32_t)t;
+    if (mode == 3) __builtin_nontemporal_store(word, rec + 64 * t + lane);
+    const uint64_t half = c0 + ((c1 - c0) / 2 & ~(uint64_t)63);
+    uint64_t c = c0 + lane;
+    for (; c + 192 < c1; c += 256) {
+        const u32x4 a = __builtin_nontemporal_load(q + c);
+        const u32x4 b = __builtin_nontemporal_load(q + c + 64);
+        const u32x4 d = __builtin_nontemporal_load(q + c + 128);
+        const u32x4 e = __builtin_nontemporal_load(q + c + 192);
+        acc ^= (a.x ^ b.y) ^ (d.z ^ e.w);
+        if (mode == 6 && c < half && c + 256 >= half)
+            __builtin_nontemporal_store(word ^ acc, rec + 64 * t + lane);
+    }
+    for (; c < c1; c += 64) {
+        const u32x4 a = __builtin_nontemporal_load(q + c);
+        acc ^= a.x ^ a.w;
+    }
+    pad[lane] = acc;
+    __builtin_amdgcn_wave_barrier();
+    acc ^= pad[lane ^ 1];
+    __builtin_amdgcn_wave_barrier();
+    const uint64_t w = word ^ acc;
+    if (mode == 1) __builtin_nontemporal_store(w, rec + 64 * t + lane);
+    else if (mode == 2) rec[64 * t + lane] = w;
+    else if (mode == 4) {
+        if (lane < 32) __builtin_nontemporal_store(u64x2{w, w ^ 1}, (u64x2*)(rec + 64 * t) + lane);
+    } else if (mode == 5) __builtin_nontemporal_store(w, ring + 64 * (t & 4095) + lane);
+    else if (mode == 7) __builtin_nontemporal_store(w, (uint64_t*)(p + 16 * c0) + lane);
+    else if (mode == 0 && acc == 0x9E3779B9u) sink[0] = acc;
+    }
+}
+
+extern "C" int rec_probe(const uint8_t* p, uint64_t bytes, uint64_t n, const uint64_t* offs,
+                         const uint32_t* lens, void* rec, void* ring, int mode, int k, int lds,
+                         uint32_t* sink, void* stream) {
+    const uint64_t tiles = (n + 63) / 64, nchunks = bytes / 16;
+    const uint64_t cpt = (nchunks + tiles - 1) / tiles;
+    const unsigned grid = (unsigned)((tiles + k - 1) / k);
+    hipStream_t s = (hipStream_t)stream;
+    if (lds == 8960)
+        hipLaunchKernelGGL(rec_probe_kernel<8960>, dim3(grid), dim3(64), 0, s, p, nchunks, cpt, n,
+                           offs, lens, (uint64_t*)rec, (uint64_t*)ring, mode, k, sink);
+    else if (lds == 7680)
+        hipLaunchKernelGGL(rec_probe_kernel<7680>, dim3(grid), dim3(64), 0, s, p, nchunks, cpt, n,
+                           offs, lens, (uint64_t*)rec, (uint64_t*)ring, mode, k, sink);
+    else
+        hipLaunchKernelGGL(rec_probe_kernel<4096>, dim3(grid), dim3(64), 0, s, p, nchunks, cpt, n,
+                           offs, lens, (uint64_t*)rec, (uint64_t*)ring, mode, k, sink);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}

@@ -54,7 +54,7 @@ def hip():
         _sig(lib, "zp_parse_batch_columns_device", i32, [vp, vp, vp, u64, vp, vp, vp, vp])
         _sig(lib, "zp_stats_device", i32, [vp, u64, vp, vp])
         _sig(lib, "zp_probe_read_device", i32, [vp, u64, vp, vp])
-        _sig(lib, "zp_probe_tiles_device", i32, [vp, u64, u64, vp, vp, vp])
+        _sig(lib, "zp_probe_tiles_device", i32, [vp, u64, u64, vp, vp, vp, vp, vp])
         _sig(lib, "zp_gen_lengths_device", i32, [i32, u64, u64, u64, vp, vp])
         _sig(lib, "zp_gen_frames_device", i32, [i32, u64, u64, u64, vp, vp, vp, vp])
         _sig(lib, "zp_reader_new", i32, [i32, vp, u64, vp])

@@ -193,9 +193,10 @@ extern "C" int zp_probe_read_device(const uint8_t* p, uint64_t bytes, uint32_t* 
 // Tile-pattern probe (diagnostic): the parse kernel's memory traffic without
 // its work. Wave t (one per workgroup, as zp_parse_kernel) reads the t-th of
 // ceil(n / 64) equal slices of the arena with nontemporal 16-B loads (four
-// in flight per lane, 1 KiB per wave instruction) and then, when `records`
-// is given, stores 64 nontemporal 8-B words at records[64 t, 64 t + 64), as
-// the parse stores the tile's records. Each wave holds as much LDS as a
+// in flight per lane, 1 KiB per wave instruction) after loading the tile's
+// 64 descriptors (when offs / lens are given) and then, when `records` is
+// given, stores 64 nontemporal 8-B words at records[64 t, 64 t + 64), as the
+// parse loads a tile's descriptors and stores its records. Each wave holds as much LDS as a
 // parse wave (sizeof(WaveLds), zp_stream.h: 18 waves per CU), so the probe
 // runs at the parse's occupancy. bench.py times it over the bench's own
 // arena and records buffer: the read-only pattern and the pattern with the
@@ -206,6 +207,8 @@ extern "C" int zp_probe_read_device(const uint8_t* p, uint64_t bytes, uint32_t* 
 __global__ void __launch_bounds__(64) zp_probe_tiles_kernel(const uint8_t* __restrict__ p,
                                                             uint64_t nchunks, uint64_t cpt,
                                                             uint64_t n,
+                                                            const uint64_t* __restrict__ offs,
+                                                            const uint32_t* __restrict__ lens,
                                                             uint64_t* __restrict__ records,
                                                             uint32_t* __restrict__ sink) {
     __shared__ uint32_t pad[PT_LDS_BYTES / 4];
@@ -215,6 +218,10 @@ __global__ void __launch_bounds__(64) zp_probe_tiles_kernel(const uint8_t* __res
     const uint64_t c1 = (t + 1) * cpt < nchunks ? (t + 1) * cpt : nchunks;
     uint64_t c = t * cpt + lane;
     uint32_t acc = 0;
+    if (offs) {                              // the tile's descriptors, as the parse loads them
+        const uint64_t i = 64 * t + lane < n ? 64 * t + lane : n - 1;
+        acc = (uint32_t)offs[i] ^ lens[i];
+    }
     for (; c + 192 < c1; c += 256) {
         const st_u32x4 a = __builtin_nontemporal_load(q + c);
         const st_u32x4 b = __builtin_nontemporal_load(q + c + 64);
@@ -238,6 +245,7 @@ __global__ void __launch_bounds__(64) zp_probe_tiles_kernel(const uint8_t* __res
 }
 
 extern "C" int zp_probe_tiles_device(const uint8_t* p, uint64_t bytes, uint64_t n,
+                                     const uint64_t* offs, const uint32_t* lens,
                                      zp_record* records, uint32_t* sink, void* stream) {
     if (!p || !sink || ((uintptr_t)p & 15) || ((uintptr_t)records & 7)) {
         snprintf(zp__errbuf(), 256, "zp_probe_tiles_device: null or unaligned pointer");
@@ -252,7 +260,8 @@ extern "C" int zp_probe_tiles_device(const uint8_t* p, uint64_t bytes, uint64_t 
     const uint64_t nchunks = bytes / 16;
     const uint64_t cpt = (nchunks + tiles - 1) / tiles;
     hipLaunchKernelGGL(zp_probe_tiles_kernel, dim3((unsigned)tiles), dim3(64), 0,
-                       (hipStream_t)stream, p, nchunks, cpt, n, (uint64_t*)records, sink);
+                       (hipStream_t)stream, p, nchunks, cpt, n, offs, lens, (uint64_t*)records,
+                       sink);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         snprintf(zp__errbuf(), 256, "zp_probe_tiles_kernel launch: %s", hipGetErrorString(e));
