@@ -1189,3 +1189,41 @@ def test_parse_one_contexts_share_the_device_server(zp):
     print(f"{len(allv)} calls: p50 {1e6 * p50:.1f} us, p99 {1e6 * p99:.1f} us, "
           f"max {1e3 * allv[-1]:.3f} ms")
     assert len(allv) == 12 * 1500 + 3 * 1500
+
+
+def test_parse_one_more_contexts_than_server_slots(zp):
+    """70 live contexts on one device: the first 64 get a slot of the device's
+    server, the rest fall back to one batch launch per call; every context's
+    answers equal the oracle's, and destroying contexts frees their slots
+    for new ones."""
+    R = zp.records
+    frames = _c5_frames(zp, 140, seed=41)
+    want = [orc.parse_one(f) for f in frames]
+    lib = zp._lib.hip()
+    rec = np.zeros(1, R.RECORD_DTYPE)
+    ext = np.zeros((2, 16), np.uint8)
+    ctxs = []
+
+    def call(ctx, i):
+        buf = ctypes.create_string_buffer(frames[i], len(frames[i]))
+        rc = lib.zp_parse_one(ctx, ctypes.addressof(buf), len(frames[i]), rec.ctypes.data,
+                              ext.ctypes.data)
+        err, wrec, wext = want[i]
+        assert rc == err and rec.tobytes() == orc.pack(wrec, wext).tobytes(), (i, rc, err)
+        assert ext.tobytes() == wext.view(np.uint8).tobytes(), i
+    try:
+        for k in range(70):
+            ctxs.append(lib.zp_ctx_create(0, 1 << 16))
+            assert ctxs[-1]
+            call(ctxs[-1], k)
+        for k, c in enumerate(ctxs):                       # all of them again, interleaved
+            call(c, 70 + k)
+        for c in ctxs[:10]:
+            lib.zp_ctx_destroy(c)
+        ctxs = ctxs[10:]
+        for k in range(10):                                # new contexts take the freed slots
+            ctxs.append(lib.zp_ctx_create(0, 1 << 16))
+            call(ctxs[-1], 130 + k)
+    finally:
+        for c in ctxs:
+            lib.zp_ctx_destroy(c)

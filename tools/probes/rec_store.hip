@@ -9,6 +9,9 @@
 //   5  nontemporal into a 2 MiB ring (L2-resident: the cost without HBM)
 //   6  nontemporal after half of the tile's loads
 //   7  nontemporal into the arena slice just read (row locality; scratch arena)
+//   8  default policy into the 2 MiB ring (stays in L2: no memory writes)
+//   9  the same bytes as 1 in two 4-B store instructions
+//  10  1 plus a second 64 x 8 B nontemporal store into the ring (two stores)
 // and per run: k consecutive tiles per wave, LDS bytes per wave (8960: the
 // parse's 18 waves per CU; 7680: 21; 4096: the VGPR bound)
 #include <hip/hip_runtime.h>
@@ -64,6 +67,14 @@ __global__ void __launch_bounds__(64) rec_probe_kernel(const uint8_t* __restrict
         if (lane < 32) __builtin_nontemporal_store(u64x2{w, w ^ 1}, (u64x2*)(rec + 64 * t) + lane);
     } else if (mode == 5) __builtin_nontemporal_store(w, ring + 64 * (t & 4095) + lane);
     else if (mode == 7) __builtin_nontemporal_store(w, (uint64_t*)(p + 16 * c0) + lane);
+    else if (mode == 8) ring[64 * (t & 4095) + lane] = w;
+    else if (mode == 9) {
+        __builtin_nontemporal_store((uint32_t)w, (uint32_t*)(rec + 64 * t) + lane);
+        __builtin_nontemporal_store((uint32_t)(w >> 32), (uint32_t*)(rec + 64 * t) + 64 + lane);
+    } else if (mode == 10) {
+        __builtin_nontemporal_store(w, rec + 64 * t + lane);
+        __builtin_nontemporal_store(w ^ 7, ring + 64 * (t & 4095) + lane);
+    }
     else if (mode == 0 && acc == 0x9E3779B9u) sink[0] = acc;
     }
 }

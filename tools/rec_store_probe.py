@@ -18,7 +18,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 MODES = {0: "no stores", 1: "nt 8 B x 64 at end (parse)", 2: "default policy at end",
          3: "nt before the loads", 4: "nt 16 B x 32 lanes", 5: "nt into a 2 MiB ring",
-         6: "nt after half the loads", 7: "nt into the arena slice just read"}
+         6: "nt after half the loads", 7: "nt into the arena slice just read",
+         8: "default policy into the 2 MiB ring", 9: "nt, two 4-B stores per lane",
+         10: "nt records + nt ring (two stores)"}
 
 
 def main():
@@ -26,8 +28,7 @@ def main():
     ap.add_argument("--config", default="c3")
     ap.add_argument("--packets", type=int, default=0)
     ap.add_argument("--rounds", type=int, default=5)
-    ap.add_argument("--variants", default="1:1:8960,3:1:8960,5:1:8960,0:1:7680,1:1:7680,"
-                    "0:1:4096,1:1:4096,0:2:8960,1:2:8960,0:4:8960,1:4:8960",
+    ap.add_argument("--variants", default="",
                     help="mode:tiles_per_wave:lds_bytes beside the modes at 1:8960")
     args = ap.parse_args()
     so = os.path.join(ROOT, "tools", "probes", "librec_store.so")
