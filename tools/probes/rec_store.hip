@@ -12,6 +12,8 @@
 //   8  default policy into the 2 MiB ring (stays in L2: no memory writes)
 //   9  the same bytes as 1 in two 4-B store instructions
 //  10  1 plus a second 64 x 8 B nontemporal store into the ring (two stores)
+//  11-14  2 / 4 / 8 / 16 nontemporal 64 x 8 B store instructions per tile into
+//      consecutive 512-B blocks of a buffer of 16 blocks per tile (`wide`)
 // and per run: k consecutive tiles per wave, LDS bytes per wave (8960: the
 // parse's 18 waves per CU; 7680: 21; 4096: the VGPR bound)
 #include <hip/hip_runtime.h>
@@ -27,7 +29,8 @@ __global__ void __launch_bounds__(64) rec_probe_kernel(const uint8_t* __restrict
                                                        const uint64_t* __restrict__ offs,
                                                        const uint32_t* __restrict__ lens,
                                                        uint64_t* __restrict__ rec,
-                                                       uint64_t* __restrict__ ring, int mode, int k,
+                                                       uint64_t* __restrict__ ring,
+                                                       uint64_t* __restrict__ wide, int mode, int k,
                                                        uint32_t* __restrict__ sink) {
     __shared__ uint32_t pad[LDSB / 4];
     const uint32_t lane = threadIdx.x;
@@ -68,6 +71,11 @@ __global__ void __launch_bounds__(64) rec_probe_kernel(const uint8_t* __restrict
     } else if (mode == 5) __builtin_nontemporal_store(w, ring + 64 * (t & 4095) + lane);
     else if (mode == 7) __builtin_nontemporal_store(w, (uint64_t*)(p + 16 * c0) + lane);
     else if (mode == 8) ring[64 * (t & 4095) + lane] = w;
+    else if (mode >= 11 && mode <= 14) {
+        const int m = 1 << (mode - 10);
+        for (int b = 0; b < m; ++b)
+            __builtin_nontemporal_store(w ^ (uint64_t)b, wide + (16 * t + b) * 64 + lane);
+    }
     else if (mode == 9) {
         __builtin_nontemporal_store((uint32_t)w, (uint32_t*)(rec + 64 * t) + lane);
         __builtin_nontemporal_store((uint32_t)(w >> 32), (uint32_t*)(rec + 64 * t) + 64 + lane);
@@ -80,7 +88,8 @@ __global__ void __launch_bounds__(64) rec_probe_kernel(const uint8_t* __restrict
 }
 
 extern "C" int rec_probe(const uint8_t* p, uint64_t bytes, uint64_t n, const uint64_t* offs,
-                         const uint32_t* lens, void* rec, void* ring, int mode, int k, int lds,
+                         const uint32_t* lens, void* rec, void* ring, void* wide, int mode, int k,
+                         int lds,
                          uint32_t* sink, void* stream) {
     const uint64_t tiles = (n + 63) / 64, nchunks = bytes / 16;
     const uint64_t cpt = (nchunks + tiles - 1) / tiles;
@@ -88,12 +97,12 @@ extern "C" int rec_probe(const uint8_t* p, uint64_t bytes, uint64_t n, const uin
     hipStream_t s = (hipStream_t)stream;
     if (lds == 8960)
         hipLaunchKernelGGL(rec_probe_kernel<8960>, dim3(grid), dim3(64), 0, s, p, nchunks, cpt, n,
-                           offs, lens, (uint64_t*)rec, (uint64_t*)ring, mode, k, sink);
+                           offs, lens, (uint64_t*)rec, (uint64_t*)ring, (uint64_t*)wide, mode, k, sink);
     else if (lds == 7680)
         hipLaunchKernelGGL(rec_probe_kernel<7680>, dim3(grid), dim3(64), 0, s, p, nchunks, cpt, n,
-                           offs, lens, (uint64_t*)rec, (uint64_t*)ring, mode, k, sink);
+                           offs, lens, (uint64_t*)rec, (uint64_t*)ring, (uint64_t*)wide, mode, k, sink);
     else
         hipLaunchKernelGGL(rec_probe_kernel<4096>, dim3(grid), dim3(64), 0, s, p, nchunks, cpt, n,
-                           offs, lens, (uint64_t*)rec, (uint64_t*)ring, mode, k, sink);
+                           offs, lens, (uint64_t*)rec, (uint64_t*)ring, (uint64_t*)wide, mode, k, sink);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }

@@ -20,7 +20,8 @@ MODES = {0: "no stores", 1: "nt 8 B x 64 at end (parse)", 2: "default policy at 
          3: "nt before the loads", 4: "nt 16 B x 32 lanes", 5: "nt into a 2 MiB ring",
          6: "nt after half the loads", 7: "nt into the arena slice just read",
          8: "default policy into the 2 MiB ring", 9: "nt, two 4-B stores per lane",
-         10: "nt records + nt ring (two stores)"}
+         10: "nt records + nt ring (two stores)", 11: "2 store instructions (wide)",
+         12: "4 store instructions", 13: "8 store instructions", 14: "16 store instructions"}
 
 
 def main():
@@ -38,14 +39,16 @@ def main():
                         "-o", so, src], check=True)
     lib = ctypes.CDLL(so)
     lib.rec_probe.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p,
-                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
-                              ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                              ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                              ctypes.c_void_p]
     zp = importlib.import_module("zero-packet_amd")
     d = torch.device("cuda:0")
     n = args.packets or {"c5": 1 << 25}.get(args.config, 1 << 24)
     a, o, l_ = zp.batch.generate(args.config, n, device=d)
     recs, ext = zp.batch.alloc_outputs(n, d)
     ring = torch.empty(64 * 4096 * 8, dtype=torch.uint8, device=d)
+    wide = torch.empty(((n + 63) // 64) * 16 * 512, dtype=torch.uint8, device=d)
     sink = torch.zeros(1, dtype=torch.int32, device=d)
     scratch = a.clone()                                   # mode 7 writes into it
     s = torch.cuda.current_stream()
@@ -59,7 +62,8 @@ def main():
         mode, k, lds = (m, 1, 8960) if isinstance(m, int) else m
         src = scratch if mode == 7 else a
         lib.rec_probe(src.data_ptr(), nb, n, o.data_ptr(), l_.data_ptr(), recs.data_ptr(),
-                      ring.data_ptr(), mode, k, lds, sink.data_ptr(), ctypes.c_void_p(s.cuda_stream))
+                      ring.data_ptr(), wide.data_ptr(), mode, k, lds, sink.data_ptr(),
+                      ctypes.c_void_p(s.cuda_stream))
     extra = [tuple(int(x) for x in v.split(":")) for v in args.variants.split(",") if v]
     keys = ["parse"] + list(MODES) + extra
     for k in keys:
