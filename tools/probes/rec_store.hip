@@ -14,6 +14,8 @@
 //  10  1 plus a second 64 x 8 B nontemporal store into the ring (two stores)
 //  11-14  2 / 4 / 8 / 16 nontemporal 64 x 8 B store instructions per tile into
 //      consecutive 512-B blocks of a buffer of 16 blocks per tile (`wide`)
+//  15 / 16  the same bytes as 1 in bigger bursts: every 4th / 16th tile's wave
+//      stores the records of 4 / 16 tiles (2 / 8 KiB), the others none
 // and per run: k consecutive tiles per wave, LDS bytes per wave (8960: the
 // parse's 18 waves per CU; 7680: 21; 4096: the VGPR bound)
 #include <hip/hip_runtime.h>
@@ -71,7 +73,13 @@ __global__ void __launch_bounds__(64) rec_probe_kernel(const uint8_t* __restrict
     } else if (mode == 5) __builtin_nontemporal_store(w, ring + 64 * (t & 4095) + lane);
     else if (mode == 7) __builtin_nontemporal_store(w, (uint64_t*)(p + 16 * c0) + lane);
     else if (mode == 8) ring[64 * (t & 4095) + lane] = w;
-    else if (mode >= 11 && mode <= 14) {
+    else if (mode == 15 || mode == 16) {
+        const uint64_t g = mode == 15 ? 4 : 16;
+        if (t % g == 0)
+            for (uint64_t b = 0; b < g; ++b)
+                if (64 * (t + b) + lane < n)
+                    __builtin_nontemporal_store(w ^ b, rec + 64 * (t + b) + lane);
+    } else if (mode >= 11 && mode <= 14) {
         const int m = 1 << (mode - 10);
         for (int b = 0; b < m; ++b)
             __builtin_nontemporal_store(w ^ (uint64_t)b, wide + (16 * t + b) * 64 + lane);

@@ -21,7 +21,8 @@ MODES = {0: "no stores", 1: "nt 8 B x 64 at end (parse)", 2: "default policy at 
          6: "nt after half the loads", 7: "nt into the arena slice just read",
          8: "default policy into the 2 MiB ring", 9: "nt, two 4-B stores per lane",
          10: "nt records + nt ring (two stores)", 11: "2 store instructions (wide)",
-         12: "4 store instructions", 13: "8 store instructions", 14: "16 store instructions"}
+         12: "4 store instructions", 13: "8 store instructions", 14: "16 store instructions",
+         15: "records of 4 tiles by every 4th wave", 16: "records of 16 tiles by every 16th"}
 
 
 def main():
