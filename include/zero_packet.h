@@ -328,23 +328,25 @@ int zp_parse_batch_host_multi(zp_ctx* const* ctxs, int nctx, const uint8_t* aren
  * parser.rs:53). ext: NULL or 2 entries (outer, ip_in_ip chain; zeroed where
  * the record flags no chain). Returns the zp_err code (>= 0) or a negative
  * value on HIP failure. The frame is copied into ctx's mapped pinned block;
- * by default a resident server wave of ctx (one wave on one CU, launched on
- * the first call) polls a doorbell there, parses the frame in place and
- * writes the record back: no kernel launch per call.
- * The wave leaves after an idle timeout (5 ms by default) without requests,
- * and after 1 ms resident whatever the traffic; the next call relaunches it
- * (under steady traffic the host queues the next wave behind the old one).
- * A device-wide synchronisation (hipDeviceSynchronize,
- * torch.cuda.synchronize, hipFree) issued meanwhile waits for the running
- * wave, so at most about 1 ms; zp_parse_one_config stops it at once.
- * Frames over 64 KiB take the batch host path. Like every zp_ctx call, one
- * thread at a time per ctx (one context per thread, or a pool). */
+ * by default the device's shared resident server (one kernel per device and
+ * process, one wave per context, launched on demand) polls a doorbell there,
+ * parses the frame in place and writes the record back: no kernel launch per
+ * call. The kernel leaves after 1 ms resident whatever
+ * the traffic; the next call replaces it (under steady traffic a caller
+ * queues the next one and retires the old one). A device-wide
+ * synchronisation (hipDeviceSynchronize, torch.cuda.synchronize, hipFree)
+ * issued meanwhile waits for the running kernel, so about 1 ms at most;
+ * zp_parse_one_config stops it at once. Frames over 64 KiB take the batch
+ * host path. Like every zp_ctx call, one thread at a time per ctx (one
+ * context per thread, or a pool); contexts of one device share the server,
+ * so their calls run concurrently. */
 int zp_parse_one(zp_ctx* ctx, const uint8_t* frame, uint64_t len,
                  zp_record* record, zp_ext_offsets ext[2]);
-/* zp_parse_one's mode on ctx: idle_us > 0 = the resident server with that
- * idle timeout (the default is 5000); 0 = one batch-kernel launch and a
- * stream wait per call (~18 us). Stops a running server either way.
- * Returns 0, or -1 on a NULL ctx. */
+/* zp_parse_one's mode on ctx: idle_us > 0 = the device's resident server
+ * (the default, 5000; the value is no longer a timeout: the server's life is
+ * 1 ms); 0 = one batch-kernel launch and a stream wait per call (~18 us).
+ * Stops the device's server either way (every context's next call
+ * relaunches it). Returns 0, or -1 on a NULL ctx. */
 int zp_parse_one_config(zp_ctx* ctx, uint32_t idle_us);
 /* The calling thread's current HIP device (hipGetDevice), -1 on failure:
  * the device a facade creates its contexts on. */

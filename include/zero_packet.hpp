@@ -533,8 +533,8 @@ public:
         if (!ctx_) throw std::runtime_error(std::string("zp_ctx_create: ") + zp_last_error());
     }
     ~Context() { zp_ctx_destroy(ctx_); }
-    // zp_parse_one's mode: idle_us > 0 = resident server (default 5000 us
-    // idle timeout), 0 = one launch per call; stops a running server.
+    // zp_parse_one's mode: idle_us > 0 = the device's resident server (the
+    // default), 0 = one launch per call; stops the device's server.
     void parse_one_mode(uint32_t idle_us) { zp_parse_one_config(ctx_, idle_us); }
     Context(const Context&) = delete;
     Context& operator=(const Context&) = delete;

@@ -640,9 +640,10 @@ POOL_MAX = 32               # pooled contexts per device; more callers wait for 
 
 class _DevicePool:
     """zp_ctx pool of one device. Frames up to ONE_MAX take a small pooled
-    context each (its own mapped block and resident server wave, so calls on
-    different threads never wait for each other); longer frames take the
-    device's one large context (256 MiB chunks) under a lock."""
+    context each (its own mapped block and slot in the device's resident
+    server, so calls on different threads never wait for each other);
+    longer frames take the device's one large context (256 MiB chunks)
+    under a lock."""
 
     def __init__(self, device):
         self.device = device
@@ -753,8 +754,8 @@ def _pool(device):
 
 
 def quiesce():
-    """Stops the resident zp_parse_one server waves of every idle context now
-    (each also leaves by itself after 5 ms without a call, and after 1 ms
+    """Stops the devices' resident zp_parse_one servers now, through the
+    idle contexts of the pools (a server also leaves by itself after 1 ms
     resident whatever the traffic; the next PacketParser.parse relaunches
     it). Call before a device-wide synchronisation to avoid waiting for
     that bound."""
