@@ -1227,3 +1227,26 @@ def test_parse_one_more_contexts_than_server_slots(zp):
     finally:
         for c in ctxs:
             lib.zp_ctx_destroy(c)
+
+
+def test_probe_tiles_stays_in_bounds(zp):
+    """zp_probe_tiles_device (bench.py's placement probe) on a batch whose
+    frame count is not a multiple of 64: the record stores stop at n (a
+    guard after the records is untouched) and the read-only form writes
+    nothing there."""
+    d = dev()
+    n = 1000
+    a, o, l_ = zp.batch.generate("c3", n, device=d)
+    buf = torch.full((n + 64, 8), 0xA5, dtype=torch.uint8, device=d)
+    sink = torch.zeros(1, dtype=torch.int32, device=d)
+    lib = zp._lib.hip()
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    nb = a.numel() // 16 * 16
+    assert lib.zp_probe_tiles_device(a.data_ptr(), nb, n, o.data_ptr(), l_.data_ptr(), None,
+                                     sink.data_ptr(), s) == 0
+    torch.cuda.synchronize()
+    assert (buf == 0xA5).all()
+    assert lib.zp_probe_tiles_device(a.data_ptr(), nb, n, o.data_ptr(), l_.data_ptr(),
+                                     buf.data_ptr(), sink.data_ptr(), s) == 0
+    torch.cuda.synchronize()
+    assert (buf[n:] == 0xA5).all() and not (buf[:n] == 0xA5).all(1).all()
