@@ -30,6 +30,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <cstring>
+#include <memory>
 #include <optional>
 #include <stdexcept>
 #include <string>
@@ -554,6 +555,23 @@ public:
 private:
     zp_ctx* ctx_;
 };
+
+// The per-frame drop-in, `zp::parse(frame)` where the reference has
+// `PacketParser::parse(frame)` (parser.rs:53): one small Context per thread
+// and device, created on first use (zp_device_current), so threads parse
+// concurrently through the device's shared resident server (INTEGRATION.md
+// §1.2). Frames over 64 KiB take the context's batch path; its 1 MiB chunk
+// refuses longer ones (use a Context with a larger chunk for jumbo traffic).
+inline PacketParser parse(Bytes frame, zp_ext_offsets* ext_out = nullptr) {
+    struct PerDevice {
+        std::unique_ptr<Context> c[64];
+    };
+    thread_local PerDevice mine;
+    const int dev = zp_device_current();
+    if (dev < 0 || dev >= 64) throw std::runtime_error(std::string("zp_device_current: ") + zp_last_error());
+    if (!mine.c[dev]) mine.c[dev] = std::make_unique<Context>(dev, 1ull << 20);
+    return mine.c[dev]->parse(frame, ext_out);
+}
 
 // A host batch over several devices (one Context each): byte-balanced
 // contiguous ranges, concurrently (zp_parse_batch_host_multi).

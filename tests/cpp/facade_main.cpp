@@ -80,6 +80,7 @@ int main(int argc, char** argv) {
     if (gpu) { std::fprintf(stderr, "built without ZP_FACADE_GPU\n"); return 2; }
 #endif
     std::string line;
+    [[maybe_unused]] uint64_t nline = 0;
     while (std::getline(std::cin, line)) {
         std::istringstream in(line);
         std::string fh, rh, eh;
@@ -90,7 +91,8 @@ int main(int argc, char** argv) {
             zp::PacketParser p;
             if (gpu) {
 #ifdef ZP_FACADE_GPU
-                p = ctx->parse(b);
+                // every other frame through the thread's implicit context
+                p = (nline++ & 1) ? zp::parse(b) : ctx->parse(b);
 #endif
             } else {
                 zp_record r{};
