@@ -261,3 +261,29 @@ def test_parse_with_columns_reused_arena_changed_traffic(zp, monkeypatch):
     assert keys[0] != keys[1], keys                      # c4 is another workload
     assert keys[0] == (4, 0, 0), keys                    # c3: all plain IPv4
     C.reset_auto()
+
+
+@pytest.mark.gpu
+def test_parse_with_columns_auto_under_graph_capture(zp):
+    """parse_with_columns(mode="auto") inside a HIP graph capture (ADVICE
+    r05): no timing events, no sampling, no synchronisation; the captured
+    launch replays to the fused path's results."""
+    import torch
+    d = torch.device("cuda:0")
+    C = zp.columns
+    C.reset_auto()
+    a, o, l_ = zp.batch.generate("c5", 1 << 14, first=8, device=d)
+    names = ["src_addr", "dest_port", "l4_proto"]
+    want_r, _, want_c = C.parse_with_columns(a, o, l_, names=names, mode="fused")
+    torch.cuda.synchronize()
+    t0 = C.auto_timings
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        r, _, c = C.parse_with_columns(a, o, l_, names=names, check=False)
+    for _ in range(2):
+        r.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(r, want_r) and all(torch.equal(c[x], want_c[x]) for x in names)
+    assert C.auto_timings == t0 and not C._shapes
+    C.reset_auto()
