@@ -167,9 +167,15 @@ def main():
         del copies
         torch.cuda.empty_cache()
     for cfg in [c for c in args.configs.split(",") if c]:
+        label = cfg
+        cfg, _, every = cfg.partition("~")         # "c3~2": every 2nd frame (gaps between frames)
         cfg, _, nn = cfg.partition(":")            # "c3:1048576": another batch size
         n = int(nn) if nn else sizes[cfg]
         arena, offs, lens = zp.batch.generate(cfg, n, device=dev)
+        if every:
+            offs, lens = offs[::int(every)].contiguous(), lens[::int(every)].contiguous()
+            n = offs.numel()
+        cfg = label
         # 16 B per frame: room for variants built with the ABI v2/v3 record
         rec = torch.empty((n, 16), dtype=torch.uint8, device=dev)
         ext = torch.empty((2, n, 16), dtype=torch.uint8, device=dev)
@@ -181,6 +187,8 @@ def main():
                 fn = lambda l=l: l.zp_parse_batch_device(arena.data_ptr(), offs.data_ptr(),
                                                           lens.data_ptr(), n, rec.data_ptr(),
                                                           ext.data_ptr(), None)
+                if r == 0:
+                    rec.fill_(0xA5)            # a build that stores no records shows as a diff
                 res[name] += time_launches(fn, args.reps)
                 if r == 0:
                     if ref is None:
