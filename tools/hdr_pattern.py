@@ -47,6 +47,9 @@ def main():
                          "frame, then the slots read back and the sectors written")
     ap.add_argument("--uncached", action="store_true",
                     help="the buffer in uncached device memory (tools/ucmem.py)")
+    ap.add_argument("--policies", default="3,1,0,2,4,5",
+                    help="store policies to time (PMC passes: one or two)")
+    ap.add_argument("--no-parse", action="store_true", help="skip the parse of 4M c3 frames")
     args = ap.parse_args()
     mb = ctypes.CDLL(os.path.join(ROOT, "tools", "libmembw.so"))
     mb.membw_hdr_tiles.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
@@ -61,9 +64,29 @@ def main():
         buf = ub
         print("buffer in uncached device memory", flush=True)
     nb = buf.numel() // args.region * args.region
+    names = {3: "read only", 1: "nt", 0: "plain", 2: "write-through", 4: "plain coop",
+             5: "write only", 6: "plain paused", 7: "coop paused"}
+    pols = [int(x) for x in args.policies.split(",")]
     for hdr in [int(x) for x in args.hdr.split(",")]:
-        for pol, name in ((3, "read only"), (1, "nt"), (0, "plain"), (2, "write-through"),
-                          (4, "plain coop"), (5, "write only")):
+        # The write floor in absolute 64-B sectors: each lane writes the
+        # 16-B chunks [s0, s1) of its tile (sectors relative to the tile base,
+        # which is only 32-B aligned for odd tiles at region 50016)
+        ntile = nb // args.region
+        base = buf.data_ptr() + np.arange(ntile, dtype=np.int64) * args.region
+        f = np.arange(64, dtype=np.int64) * (args.region // 64)
+        s0, s1 = f & ~63, (f + hdr + 63) & ~63
+        s1 = np.minimum(s1, args.region // 16 * 16)
+        lo = (base[:, None] + s0[None, :]) // 64
+        hi = (base[:, None] + s1[None, :] - 1) // 64
+        sect = int((hi - lo + 1).sum())
+        part = int(((base[:, None] + s0[None, :]) % 64 != 0).sum() +
+                   ((base[:, None] + s1[None, :]) % 64 != 0).sum())
+        wbytes = int((s1 - s0).sum()) * ntile
+        print(f"hdr {hdr}: {ntile} tiles, written {wbytes / 1e6:.1f} MB in {sect} absolute 64-B "
+              f"sectors = {sect * 64 / 1e6:.1f} MB ({part} partially covered sector ends)",
+              flush=True)
+        for pol in pols:
+            name = names[pol]
             ms = timed(lambda: mb.membw_hdr_tiles(buf.data_ptr(), buf.numel(), args.region, hdr,
                                                   pol, 13 * 1024, None))
             print(f"hdr tiles region {args.region} hdr {hdr:4d} B {name:14s}: {ms:7.3f} ms "
@@ -80,6 +103,8 @@ def main():
                 print(f"hdr tiles region {args.region} hdr {hdr:4d} B {name:14s}: {ms:7.3f} ms",
                       flush=True)
         del tmp
+    if args.no_parse:
+        return
     zp = importlib.import_module("zero-packet_amd")
     n = 1 << 22
     arena, offs, lens = zp.batch.generate("c3", n, device=d)

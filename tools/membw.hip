@@ -358,7 +358,9 @@ extern "C" int membw_copy_gap(const void* src, void* dst, uint64_t bytes, int ga
 // the builder's header write-back does. policy: 0 plain stores, 1
 // nontemporal, 2 write-through (sc1, system-coherent scope bit), 3 no write,
 // 4 plain stores by the whole wave (frame-major, coalesced), 5 plain stores
-// without the read.
+// without the read, 6 / 7 = 0 / 4 after a ~12 us pause between the read and
+// the write-back (the builder's chains run there: are the tile's lines still
+// in L2 when its header sectors are written?).
 template <int POLICY>
 __global__ void __launch_bounds__(64) hdr_tiles(uint8_t* __restrict__ p, uint64_t region,
                                                 uint32_t hdr, uint32_t lds_bytes) {
@@ -383,12 +385,15 @@ __global__ void __launch_bounds__(64) hdr_tiles(uint8_t* __restrict__ p, uint64_
     lds[lane] = acc;
     __builtin_amdgcn_wave_barrier();
     acc += lds[(lane + 1) & 63] + lds_bytes;
+    if (POLICY >= 6) {
+        for (int k = 0; k < 3; ++k) __builtin_amdgcn_s_sleep(127);
+    }
     if (POLICY == 3) {
         if (acc == 0x12345678u) base[0] = 1;
         return;
     }
     u32x4 val = {acc, acc ^ 1u, acc ^ 2u, acc ^ 3u};
-    if (POLICY == 4) {
+    if (POLICY == 4 || POLICY == 7) {
         // wave-cooperative: the 64 frames' sector ranges as one linear list of
         // 16-B chunks, consecutive lanes on consecutive chunks of a frame
         const uint32_t cmax = ((hdr + 63) / 64 + 1) * 4;
@@ -405,7 +410,7 @@ __global__ void __launch_bounds__(64) hdr_tiles(uint8_t* __restrict__ p, uint64_
     const uint64_t s0 = f & ~63ull, s1 = (f + hdr + 63) & ~63ull;
     for (uint64_t a = s0; a < s1 && a + 16 <= region; a += 16) {
         __attribute__((address_space(1))) u32x4* q = (__attribute__((address_space(1))) u32x4*)(base + a);
-        if (POLICY == 0 || POLICY == 5) *q = val;
+        if (POLICY == 0 || POLICY == 5 || POLICY == 6) *q = val;
         else if (POLICY == 1) __builtin_nontemporal_store(val, q);
         else __hip_atomic_store((__attribute__((address_space(1))) uint64_t*)q, ((uint64_t)val.y << 32) | val.x,
                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
@@ -476,6 +481,8 @@ extern "C" int membw_hdr_tiles(void* p, uint64_t bytes, uint64_t region, uint32_
     case 2: hipLaunchKernelGGL(hdr_tiles<2>, dim3((unsigned)nreg), dim3(64), lds_bytes, s, q, region, hdr, lds_bytes); break;
     case 4: hipLaunchKernelGGL(hdr_tiles<4>, dim3((unsigned)nreg), dim3(64), lds_bytes, s, q, region, hdr, lds_bytes); break;
     case 5: hipLaunchKernelGGL(hdr_tiles<5>, dim3((unsigned)nreg), dim3(64), lds_bytes, s, q, region, hdr, lds_bytes); break;
+    case 6: hipLaunchKernelGGL(hdr_tiles<6>, dim3((unsigned)nreg), dim3(64), lds_bytes, s, q, region, hdr, lds_bytes); break;
+    case 7: hipLaunchKernelGGL(hdr_tiles<7>, dim3((unsigned)nreg), dim3(64), lds_bytes, s, q, region, hdr, lds_bytes); break;
     default: hipLaunchKernelGGL(hdr_tiles<3>, dim3((unsigned)nreg), dim3(64), lds_bytes, s, q, region, hdr, lds_bytes); break;
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;
