@@ -65,7 +65,8 @@ def main():
         print("buffer in uncached device memory", flush=True)
     nb = buf.numel() // args.region * args.region
     names = {3: "read only", 1: "nt", 0: "plain", 2: "write-through", 4: "plain coop",
-             5: "write only", 6: "plain paused", 7: "coop paused"}
+             5: "write only", 6: "plain paused", 7: "coop paused",
+             8: "at frame start", 9: "at frame end"}
     pols = [int(x) for x in args.policies.split(",")]
     for hdr in [int(x) for x in args.hdr.split(",")]:
         # The write floor in absolute 64-B sectors: each lane writes the

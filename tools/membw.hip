@@ -361,6 +361,9 @@ extern "C" int membw_copy_gap(const void* src, void* dst, uint64_t bytes, int ga
 // without the read, 6 / 7 = 0 / 4 after a ~12 us pause between the read and
 // the write-back (the builder's chains run there: are the tile's lines still
 // in L2 when its header sectors are written?).
+// 8: each lane writes its sectors right after the group of loads holding its
+// frame's start, 9: after the group holding its frame's end (a builder that
+// writes a frame back as the stream passes it: the DRAM rows just read).
 template <int POLICY>
 __global__ void __launch_bounds__(64) hdr_tiles(uint8_t* __restrict__ p, uint64_t region,
                                                 uint32_t hdr, uint32_t lds_bytes) {
@@ -381,7 +384,19 @@ __global__ void __launch_bounds__(64) hdr_tiles(uint8_t* __restrict__ p, uint64_
         }
 #pragma unroll
         for (int q = 0; q < 8; ++q) acc += v[q].x ^ v[q].y ^ v[q].z ^ v[q].w;
+        if (POLICY == 8 || POLICY == 9) {
+            const uint64_t g0 = i * 1024, g1 = g0 + 8 * 1024;
+            const uint64_t f = (uint64_t)lane * (region / 64);
+            const uint64_t at = POLICY == 8 ? f : f + region / 64 - 1;
+            if (at >= g0 && at < g1) {
+                const u32x4 val = {acc, acc ^ 1u, acc ^ 2u, acc ^ 3u};
+                const uint64_t s0 = f & ~63ull, s1 = (f + hdr + 63) & ~63ull;
+                for (uint64_t a = s0; a < s1 && a + 16 <= region; a += 16)
+                    *(__attribute__((address_space(1))) u32x4*)(base + a) = val;
+            }
+        }
     }
+    if (POLICY == 8 || POLICY == 9) return;
     lds[lane] = acc;
     __builtin_amdgcn_wave_barrier();
     acc += lds[(lane + 1) & 63] + lds_bytes;
@@ -483,6 +498,8 @@ extern "C" int membw_hdr_tiles(void* p, uint64_t bytes, uint64_t region, uint32_
     case 5: hipLaunchKernelGGL(hdr_tiles<5>, dim3((unsigned)nreg), dim3(64), lds_bytes, s, q, region, hdr, lds_bytes); break;
     case 6: hipLaunchKernelGGL(hdr_tiles<6>, dim3((unsigned)nreg), dim3(64), lds_bytes, s, q, region, hdr, lds_bytes); break;
     case 7: hipLaunchKernelGGL(hdr_tiles<7>, dim3((unsigned)nreg), dim3(64), lds_bytes, s, q, region, hdr, lds_bytes); break;
+    case 8: hipLaunchKernelGGL(hdr_tiles<8>, dim3((unsigned)nreg), dim3(64), lds_bytes, s, q, region, hdr, lds_bytes); break;
+    case 9: hipLaunchKernelGGL(hdr_tiles<9>, dim3((unsigned)nreg), dim3(64), lds_bytes, s, q, region, hdr, lds_bytes); break;
     default: hipLaunchKernelGGL(hdr_tiles<3>, dim3((unsigned)nreg), dim3(64), lds_bytes, s, q, region, hdr, lds_bytes); break;
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;
