@@ -16,6 +16,10 @@
 //      consecutive 512-B blocks of a buffer of 16 blocks per tile (`wide`)
 //  15 / 16  the same bytes as 1 in bigger bursts: every 4th / 16th tile's wave
 //      stores the records of 4 / 16 tiles (2 / 8 KiB), the others none
+//  17 / 18  64 lanes x 4 B / 2 B nontemporal at the end (a 4-B / 2-B record:
+//      does the cost follow the bytes?)
+//  19  the low 4 B of each 8-B record only (stride 8: the same lines, half
+//      the bytes); 20: 19, plus the high 4 B for every 4th lane
 // and per run: k consecutive tiles per wave, LDS bytes per wave (8960: the
 // parse's 18 waves per CU; 7680: 21; 4096: the VGPR bound)
 #include <hip/hip_runtime.h>
@@ -83,6 +87,13 @@ __global__ void __launch_bounds__(64) rec_probe_kernel(const uint8_t* __restrict
         const int m = 1 << (mode - 10);
         for (int b = 0; b < m; ++b)
             __builtin_nontemporal_store(w ^ (uint64_t)b, wide + (16 * t + b) * 64 + lane);
+    }
+    else if (mode == 17) __builtin_nontemporal_store((uint32_t)w, (uint32_t*)(rec + 64 * t) + lane);
+    else if (mode == 18) __builtin_nontemporal_store((uint16_t)w, (uint16_t*)(rec + 64 * t) + lane);
+    else if (mode == 19 || mode == 20) {
+        __builtin_nontemporal_store((uint32_t)w, (uint32_t*)(rec + 64 * t + lane));
+        if (mode == 20 && (lane & 3) == 0)
+            __builtin_nontemporal_store((uint32_t)(w >> 32), (uint32_t*)(rec + 64 * t + lane) + 1);
     }
     else if (mode == 9) {
         __builtin_nontemporal_store((uint32_t)w, (uint32_t*)(rec + 64 * t) + lane);

@@ -22,7 +22,9 @@ MODES = {0: "no stores", 1: "nt 8 B x 64 at end (parse)", 2: "default policy at 
          8: "default policy into the 2 MiB ring", 9: "nt, two 4-B stores per lane",
          10: "nt records + nt ring (two stores)", 11: "2 store instructions (wide)",
          12: "4 store instructions", 13: "8 store instructions", 14: "16 store instructions",
-         15: "records of 4 tiles by every 4th wave", 16: "records of 16 tiles by every 16th"}
+         15: "records of 4 tiles by every 4th wave", 16: "records of 16 tiles by every 16th",
+         17: "nt 4 B x 64 at end (a 4-B record)", 18: "nt 2 B x 64 at end (a 2-B record)",
+         19: "nt low 4 B of each 8-B record", 20: "19 + high 4 B for every 4th lane"}
 
 
 def main():
@@ -30,6 +32,7 @@ def main():
     ap.add_argument("--config", default="c3")
     ap.add_argument("--packets", type=int, default=0)
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--modes", default="", help="comma list of modes (default: all)")
     ap.add_argument("--variants", default="",
                     help="mode:tiles_per_wave:lds_bytes beside the modes at 1:8960")
     args = ap.parse_args()
@@ -66,7 +69,10 @@ def main():
                       ring.data_ptr(), wide.data_ptr(), mode, k, lds, sink.data_ptr(),
                       ctypes.c_void_p(s.cuda_stream))
     extra = [tuple(int(x) for x in v.split(":")) for v in args.variants.split(",") if v]
-    keys = ["parse"] + list(MODES) + extra
+    modes = [int(x) for x in args.modes.split(",") if x] or list(MODES)
+    if 0 not in modes:
+        modes = [0] + modes
+    keys = ["parse"] + modes + extra
     for k in keys:
         run(k)
     ms = {k: [] for k in keys}
