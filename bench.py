@@ -215,7 +215,11 @@ def placement_probe(zp, arena, offs, lens, records, kernel_ms, reps=5):
                 tile's descriptors, then its slice of the arena);
       tiles_rec the same plus the 8-B record stores into the bench's records
                 buffer: tiles_rec - tiles is what the record stores cost on
-                this records placement.
+                this records placement (DESIGN.md §4);
+      tiles_code the same with record codes (zp_probe_tiles_codes_device: a
+                byte per frame, then the expansion kernel), the pattern of
+                the parse when it stores codes (zp_set_record_slots, the
+                automatic mode from 2M frames).
     parse_over_* = the parse kernel's mean time / the probe's."""
     import ctypes
     lib = zp._lib.hip()
@@ -231,6 +235,9 @@ def placement_probe(zp, arena, offs, lens, records, kernel_ms, reps=5):
                                                    sink.data_ptr(), s),
         "tiles_rec": lambda: lib.zp_probe_tiles_device(arena.data_ptr(), nb, n, od, ld,
                                                        records.data_ptr(), sink.data_ptr(), s),
+        "tiles_code": lambda: lib.zp_probe_tiles_codes_device(arena.data_ptr(), nb, n, od, ld,
+                                                              records.data_ptr(), sink.data_ptr(),
+                                                              s),
     }
     for f in probes.values():
         zp._lib.check(f(), "placement probe")
@@ -251,12 +258,15 @@ def placement_probe(zp, arena, offs, lens, records, kernel_ms, reps=5):
             "parse_over_read": round(kernel_ms / med["read"], 4),
             "parse_over_tiles": round(kernel_ms / med["tiles"], 4),
             "parse_over_tiles_rec": round(kernel_ms / med["tiles_rec"], 4),
+            "tiles_code_ms": round(med["tiles_code"], 4),
+            "parse_over_tiles_code": round(kernel_ms / med["tiles_code"], 4),
             "arena_va_mod_1g": arena.data_ptr() % (1 << 30),
             "records_va_mod_1g": records.data_ptr() % (1 << 30),
             "probe": "zp_probe_read_device: grid-stride nt 16-B loads, 2048 x 256 lanes; "
                      "zp_probe_tiles_device: one wave per 64-frame slice, its 64 descriptors, "
                      "nt 16-B loads, tiles_rec + 64 nt 8-B stores per wave into the bench's "
-                     "records"}
+                     "records; zp_probe_tiles_codes_device: tiles + a 64-B code store per full "
+                     "tile, then the record expansion kernel"}
 
 
 def gather_rows(row, world, rank, dev):

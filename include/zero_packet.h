@@ -303,6 +303,21 @@ int zp_parse_batch_device(const uint8_t* arena, const uint64_t* offs,
                           zp_record* records, zp_ext_offsets* ext,
                           void* stream);
 
+/*
+ * Record codes (round 6). Inside the parse's read stream a record store
+ * costs in proportion to the contiguous bytes a wave stores,
+ * so a full tile of 64 frames whose records all have the common form (no
+ * error, no IP-in-IP, no extension headers, the L4 reader right after a
+ * 20-B IPv4 or 40-B IPv6 header: config 3) is stored as one code byte per
+ * frame over the tile's first 8 records, and a second kernel on the same
+ * stream rewrites the tile's 64 records from the codes. The records a
+ * caller reads are the same either way (zp_parse_batch_device still only
+ * enqueues). mode 0: automatic (batches of at least 2,097,152 frames),
+ * 1: always, 2: never. Process-wide; returns the previous mode, or -1 for
+ * an unknown mode.
+ */
+int zp_set_record_slots(int mode);
+
 /* Host-buffer convenience path: the frames, descriptors and outputs live in
  * host memory (a NIC ring / raw socket buffer). Stages through pinned buffers
  * and overlaps H2D copy, parse and D2H copy in chunks on `ctx`'s streams.
@@ -440,6 +455,12 @@ int zp_probe_read_device(const uint8_t* p, uint64_t bytes, uint32_t* sink, void*
 int zp_probe_tiles_device(const uint8_t* p, uint64_t bytes, uint64_t n, const uint64_t* offs,
                           const uint32_t* lens, zp_record* records, uint32_t* sink,
                           void* stream);
+/* Diagnostic: the same pattern with record codes (zp_set_record_slots): a
+ * full tile stores one byte per frame instead of its 8-B records and the
+ * parse's expansion kernel then rewrites records [0, n) (junk contents). */
+int zp_probe_tiles_codes_device(const uint8_t* p, uint64_t bytes, uint64_t n,
+                                const uint64_t* offs, const uint32_t* lens, zp_record* records,
+                                uint32_t* sink, void* stream);
 
 /* ------------------------------------------------------------------------- */
 /* Host-ring ingestion pipeline. Frames start in host */

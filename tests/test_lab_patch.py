@@ -73,7 +73,7 @@ def test_lab_default_build_is_the_product(tmp_path):
                 assert re.search(r"#\s*define\s+" + ident + r"\b", text), (name, ident)
     jobs = {}
     for tag, root in (("product", CSRC), ("lab", str(lab))):
-        for src in ("zp_parse.hip", "zp_build.hip"):
+        for src in ("zp_parse.hip", "zp_parse_slots.hip", "zp_build.hip"):
             out = str(tmp_path / f"{tag}_{src}.s")
             jobs[(tag, src)] = (out, subprocess.Popen(
                 [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
@@ -81,7 +81,7 @@ def test_lab_default_build_is_the_product(tmp_path):
                 stdout=subprocess.DEVNULL, stderr=subprocess.PIPE))
     for out, p in jobs.values():
         assert p.wait(timeout=600) == 0, p.stderr.read()
-    for src in ("zp_parse.hip", "zp_build.hip"):
+    for src in ("zp_parse.hip", "zp_parse_slots.hip", "zp_build.hip"):
         a = _kernels(open(jobs[("product", src)][0]).read())
         b = _kernels(open(jobs[("lab", src)][0]).read())
         assert a and set(a) == set(b), src

@@ -1,0 +1,154 @@
+"""Record codes (zp_set_record_slots, round 6): a full tile whose 64 records
+all have the common form is stored by the parse kernel as one code byte per
+frame and rewritten to its 64 records by zp_rec_expand_kernel. The records a
+caller sees must be byte-identical to the oracle's and to the code-free
+path's in every case: tiles with codes, tiles that lose them at the
+checksum verdict, tiles of 64-B frames (the register path), ragged last
+tiles, prior garbage in the records buffer, and the automatic mode at full
+size."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+import oracle as orc
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_slot_mode_switch_cpu(built):
+    """The switch is host state only (no GPU needed): returns the previous
+    mode and refuses unknown ones."""
+    lib = ctypes.CDLL(os.path.join(ROOT, "zero-packet_amd", "libzp_hip.so"))
+    lib.zp_set_record_slots.argtypes = [ctypes.c_int]
+    prev = lib.zp_set_record_slots(2)
+    assert prev in (0, 1, 2)
+    assert lib.zp_set_record_slots(1) == 2
+    assert lib.zp_set_record_slots(3) == -1 and lib.zp_set_record_slots(-1) == -1
+    assert lib.zp_set_record_slots(prev) == 1
+
+
+torch = pytest.importorskip("torch")
+
+
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    return torch.device("cuda:0")
+
+
+@pytest.fixture
+def slots(zp):
+    lib = zp._lib.hip()
+    prev = lib.zp_set_record_slots(0)
+    yield lambda mode: lib.zp_set_record_slots(mode)
+    lib.zp_set_record_slots(prev)
+
+
+def parse_modes(zp, slots, a, o, l_, fill=None):
+    """Records under slots always (1) and never (2), as numpy (n, 8) bytes."""
+    d = dev()
+    at = torch.from_numpy(np.asarray(a, np.uint8)).to(d) if isinstance(a, np.ndarray) else a
+    ot = torch.from_numpy(np.asarray(o, np.int64)).to(d) if isinstance(o, np.ndarray) else o
+    lt = torch.from_numpy(np.asarray(l_, np.uint32).astype(np.int32)).to(d) \
+        if isinstance(l_, np.ndarray) else l_
+    out = {}
+    for mode in (1, 2):
+        slots(mode)
+        n = ot.numel()
+        rec = torch.empty((n, 8), dtype=torch.uint8, device=d)
+        rec.fill_(0xFF if fill is None else fill)
+        ext = torch.zeros((2, n, 16), dtype=torch.uint8, device=d)
+        r, e = zp.batch.parse_batch(at, ot, lt, rec, ext)
+        torch.cuda.synchronize()
+        out[mode] = zp.batch.records_to_numpy(r, e)
+    return out
+
+
+def check(zp, out, a, o, l_):
+    want, wext = orc.parse_batch(np.asarray(a), np.asarray(o, np.uint64), np.asarray(l_, np.uint32))
+    w = orc.pack(want, wext).view(np.uint8).reshape(-1, 8)
+    for mode, (got, gext) in out.items():
+        g = got.view(np.uint8).reshape(-1, 8)
+        diff = np.nonzero((g != w).any(1))[0]
+        assert len(diff) == 0, (mode, len(diff), diff[:5])
+        assert zp.records.ext_match(gext, wext, want)
+    return want
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg,n", [("c1", 64 * 200 + 5), ("c3", 64 * 400 + 63), ("c4", 64 * 300),
+                                   ("c5", 64 * 500 + 1), ("c6", 64 * 400 + 30)])
+def test_slots_configs_exact(zp, slots, cfg, n):
+    arena, offs, lens = zp.batch.generate(cfg, n, first=777, device=dev())
+    a, o, l_ = arena.cpu().numpy(), offs.cpu().numpy(), lens.cpu().numpy()
+    out = parse_modes(zp, slots, arena, offs, lens)
+    want = check(zp, out, a, o, l_)
+    assert (want["err"] == 0).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fill", [0x00, 0xFF, 0xA5])
+def test_slots_verdict_changes_the_tile(zp, slots, fill):
+    """c3 tiles built to reach every branch of the code decision: a tile
+    whose walk records all have codes and whose verdict fails one frame's L4
+    checksum (the records are stored after the verdict, without codes); a
+    tile with an IPv4 header checksum error from the walk plus an L4 failure
+    from the verdict and tiles with several walk errors (stored before the
+    verdict); untouched tiles (codes). Any prior contents of the records
+    buffer."""
+    n = 64 * 64
+    arena, offs, lens = zp.batch.generate("c3", n, first=31337, device=dev())
+    a, o, l_ = arena.cpu().numpy().copy(), offs.cpu().numpy(), lens.cpu().numpy()
+    rng = np.random.default_rng(3)
+    for t in range(64):
+        base = 64 * t
+        kind = t % 4
+        if kind == 1:                            # one L4 checksum failure
+            i = base + int(rng.integers(0, 64))
+            a[int(o[i]) + int(l_[i]) - 1] ^= 1
+        elif kind == 2:                          # IPv4 header checksum + an L4 failure
+            i, j = base + 3, base + 40
+            a[int(o[i]) + 24] ^= 0x10             # header checksum byte
+            a[int(o[j]) + int(l_[j]) - 1] ^= 2
+        elif kind == 3:                          # many walk errors
+            for k in range(6):
+                i = base + 5 * k + 1
+                a[int(o[i]) + [12, 14, 16, 22, 24, 47][k]] ^= 0x40
+    out = parse_modes(zp, slots, a, o, l_, fill=fill)
+    want = check(zp, out, a, o, l_)
+    errs = want["err"].reshape(64, 64)
+    assert (errs[1::4] != 0).sum(1).min() == 1
+    assert all(len(np.unique(errs[t])) >= 3 for t in range(2, 64, 4))
+
+
+@pytest.mark.gpu
+def test_slots_min_size_tiles(zp, slots):
+    """Tiles of 64-B frames take the register path, which stores codes too;
+    a flipped bit sends its tile to the stream path."""
+    n = 64 * 300 + 17
+    arena, offs, lens = zp.batch.generate("c1", n, first=4, device=dev())
+    a, o, l_ = arena.cpu().numpy().copy(), offs.cpu().numpy(), lens.cpu().numpy()
+    rng = np.random.default_rng(9)
+    for i in rng.choice(n, 40, replace=False):
+        a[int(o[i]) + int(rng.integers(0, 64))] ^= np.uint8(1 << int(rng.integers(0, 8)))
+    out = parse_modes(zp, slots, a, o, l_)
+    check(zp, out, a, o, l_)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", ["c3", "c5"])
+def test_slots_auto_mode_full_size(zp, slots, cfg):
+    """The automatic mode takes codes from 2,097,152 frames on: 4M frames
+    parse to the same bytes with codes (auto) and without (never)."""
+    n = 4 << 20
+    arena, offs, lens = zp.batch.generate(cfg, n, device=dev())
+    got = {}
+    for mode in (0, 2):
+        slots(mode)
+        rec = torch.full((n, 8), 0xFF, dtype=torch.uint8, device=arena.device)
+        r, _ = zp.batch.parse_batch(arena, offs, lens, rec, check=False)
+        torch.cuda.synchronize()
+        got[mode] = r
+    assert torch.equal(got[0], got[2])
+    assert int((zp.batch.record_err(got[0]) != 0).sum()) == 0

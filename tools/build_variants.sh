@@ -14,17 +14,17 @@ C=$S/zero-packet_amd/csrc
 build() {  # name flags...
   local name=$1; shift
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared "$@" \
-     -o tools/variants/libzp_$name.so $C/zp_parse.hip || exit 1
+     -o tools/variants/libzp_$name.so $C/zp_parse.hip $C/zp_parse_slots.hip || exit 1
 }
 buildb() {  # builder variants: name flags...
   local name=$1; shift
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared "$@" \
-     -o tools/variants/libzb_$name.so $C/zp_build.hip $C/zp_parse.hip || exit 1
+     -o tools/variants/libzb_$name.so $C/zp_build.hip $C/zp_parse.hip $C/zp_parse_slots.hip || exit 1
 }
 buildc() {  # column-view variants (parse + fields): name flags...
   local name=$1; shift
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared "$@" \
-     -o tools/variants/libzc_$name.so $C/zp_fields.hip $C/zp_parse.hip || exit 1
+     -o tools/variants/libzc_$name.so $C/zp_fields.hip $C/zp_parse.hip $C/zp_parse_slots.hip || exit 1
 }
 for v in "$@"; do
   case $v in

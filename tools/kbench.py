@@ -51,7 +51,16 @@ def main():
     zp = importlib.import_module("zero-packet_amd")
     dev = torch.device("cuda:0")
     libs = {} if args.no_base else {"base": zp._lib.hip()}
+    slot_mode = {}
     for v in [x for x in args.variants.split(",") if x]:
+        if "@" in v:                               # "<lib>@<mode>": zp_set_record_slots(mode)
+            base_v, m = v.split("@")
+            l = libs["base"] if base_v == "base" else ctypes.CDLL(
+                os.path.join(ROOT, "tools", "variants", f"libzp_{base_v}.so"))
+            l.zp_set_record_slots.argtypes = [ctypes.c_int]
+            libs[v] = l
+            slot_mode[v] = int(m)
+            continue
         so = os.path.join(ROOT, "tools", "variants", f"libzp_{v}.so")
         l = ctypes.CDLL(so)
         l.zp_parse_batch_device.restype = ctypes.c_int
@@ -187,6 +196,8 @@ def main():
                 fn = lambda l=l: l.zp_parse_batch_device(arena.data_ptr(), offs.data_ptr(),
                                                           lens.data_ptr(), n, rec.data_ptr(),
                                                           ext.data_ptr(), None)
+                if hasattr(l, "zp_set_record_slots"):
+                    l.zp_set_record_slots(slot_mode.get(name, 0))
                 if r == 0:
                     rec.fill_(0xA5)            # a build that stores no records shows as a diff
                 res[name] += time_launches(fn, args.reps)

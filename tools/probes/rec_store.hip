@@ -20,6 +20,8 @@
 //      does the cost follow the bytes?)
 //  19  the low 4 B of each 8-B record only (stride 8: the same lines, half
 //      the bytes); 20: 19, plus the high 4 B for every 4th lane
+//  21  a 64-B compressed tile slot (16 lanes x 4 B) at the start of the
+//      tile's record block; 22: the same slot as 4 lanes x 16 B
 // and per run: k consecutive tiles per wave, LDS bytes per wave (8960: the
 // parse's 18 waves per CU; 7680: 21; 4096: the VGPR bound)
 #include <hip/hip_runtime.h>
@@ -90,6 +92,11 @@ __global__ void __launch_bounds__(64) rec_probe_kernel(const uint8_t* __restrict
     }
     else if (mode == 17) __builtin_nontemporal_store((uint32_t)w, (uint32_t*)(rec + 64 * t) + lane);
     else if (mode == 18) __builtin_nontemporal_store((uint16_t)w, (uint16_t*)(rec + 64 * t) + lane);
+    else if (mode == 21) {
+        if (lane < 16) __builtin_nontemporal_store((uint32_t)w, (uint32_t*)(rec + 64 * t) + lane);
+    } else if (mode == 22) {
+        if (lane < 4) __builtin_nontemporal_store(u64x2{w, w ^ 3}, (u64x2*)(rec + 64 * t) + lane);
+    }
     else if (mode == 19 || mode == 20) {
         __builtin_nontemporal_store((uint32_t)w, (uint32_t*)(rec + 64 * t + lane));
         if (mode == 20 && (lane & 3) == 0)
@@ -123,5 +130,26 @@ extern "C" int rec_probe(const uint8_t* p, uint64_t bytes, uint64_t n, const uin
     else
         hipLaunchKernelGGL(rec_probe_kernel<4096>, dim3(grid), dim3(64), 0, s, p, nchunks, cpt, n,
                            offs, lens, (uint64_t*)rec, (uint64_t*)ring, (uint64_t*)wide, mode, k, sink);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+// The expansion pass of a compressed-slot scheme: one wave per tile reads the
+// tile's 64-B slot (lane l: dword l & 15) and writes the tile's 64 8-B records.
+__global__ void __launch_bounds__(256) expand_probe_kernel(uint64_t* __restrict__ rec, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint64_t t = i / 64;
+    const uint32_t lane = threadIdx.x & 63;
+    if (64 * t >= n) return;
+    const uint32_t d = ((const uint32_t*)(rec + 64 * t))[lane & 15];
+    const uint32_t m = __shfl(d, 0);
+    const uint32_t ix = (__shfl(d, 10 + (lane >> 4)) >> (2 * (lane & 15))) & 3u;
+    const uint32_t lo = __shfl(d, 2 + 2 * ix), hi = __shfl(d, 3 + 2 * ix);
+    if (m == 0xFFFFFFFFu) return;                       // (never in the probe)
+    if (i < n) __builtin_nontemporal_store(((uint64_t)hi << 32) | lo, rec + i);
+}
+extern "C" int expand_probe(void* rec, uint64_t n, void* stream) {
+    const unsigned grid = (unsigned)((n + 255) / 256);
+    hipLaunchKernelGGL(expand_probe_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                       (uint64_t*)rec, n);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }

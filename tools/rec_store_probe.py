@@ -24,7 +24,9 @@ MODES = {0: "no stores", 1: "nt 8 B x 64 at end (parse)", 2: "default policy at 
          12: "4 store instructions", 13: "8 store instructions", 14: "16 store instructions",
          15: "records of 4 tiles by every 4th wave", 16: "records of 16 tiles by every 16th",
          17: "nt 4 B x 64 at end (a 4-B record)", 18: "nt 2 B x 64 at end (a 2-B record)",
-         19: "nt low 4 B of each 8-B record", 20: "19 + high 4 B for every 4th lane"}
+         19: "nt low 4 B of each 8-B record", 20: "19 + high 4 B for every 4th lane",
+         21: "64-B slot per tile, 16 x 4 B", 22: "64-B slot per tile, 4 x 16 B",
+         "x": "expansion pass alone (slot -> 64 records)", "21x": "mode 21 + expansion pass"}
 
 
 def main():
@@ -59,7 +61,14 @@ def main():
     nb = a.numel() // 16 * 16
     nbytes = int(l_.to(torch.int64).sum())
 
+    lib.expand_probe.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
+
     def run(m):
+        if m in ("x", "21x"):
+            if m == "21x":
+                run(21)
+            lib.expand_probe(recs.data_ptr(), n, ctypes.c_void_p(s.cuda_stream))
+            return
         if m == "parse":
             zp.batch.parse_batch(a, o, l_, recs, ext, check=False)
             return
@@ -69,7 +78,7 @@ def main():
                       ring.data_ptr(), wide.data_ptr(), mode, k, lds, sink.data_ptr(),
                       ctypes.c_void_p(s.cuda_stream))
     extra = [tuple(int(x) for x in v.split(":")) for v in args.variants.split(",") if v]
-    modes = [int(x) for x in args.modes.split(",") if x] or list(MODES)
+    modes = [x if x in ("x", "21x") else int(x) for x in args.modes.split(",") if x] or list(MODES)
     if 0 not in modes:
         modes = [0] + modes
     keys = ["parse"] + modes + extra
@@ -91,7 +100,7 @@ def main():
     for k in keys:
         med = float(np.median(ms[k]))
         name = "parse (zp_parse_kernel)" if k == "parse" else \
-            f"mode {k}: {MODES[k]}" if isinstance(k, int) else \
+            f"mode {k}: {MODES[k]}" if isinstance(k, (int, str)) else \
             f"mode {k[0]}, {k[1]} tiles/wave, {k[2]} B LDS"
         print(f"  {name:42s} {med:8.4f} ms  {nbytes / (med * 1e-3) / 1e9:7.1f} GB/s  "
               f"+{med - base:7.4f} ms over no stores", flush=True)

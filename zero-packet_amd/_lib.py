@@ -38,6 +38,7 @@ def hip():
         _sig(lib, "zp_err_str", ctypes.c_char_p, [i32])
         _sig(lib, "zp_last_error", ctypes.c_char_p, [])
         _sig(lib, "zp_parse_batch_device", i32, [vp, vp, vp, u64, vp, vp, vp])
+        _sig(lib, "zp_set_record_slots", i32, [i32])
         _sig(lib, "zp_ctx_create", vp, [i32, u64])
         _sig(lib, "zp_ctx_destroy", None, [vp])
         _sig(lib, "zp_parse_batch_host", i32, [vp, vp, u64, vp, vp, u64, vp, vp])
@@ -55,6 +56,7 @@ def hip():
         _sig(lib, "zp_stats_device", i32, [vp, u64, vp, vp])
         _sig(lib, "zp_probe_read_device", i32, [vp, u64, vp, vp])
         _sig(lib, "zp_probe_tiles_device", i32, [vp, u64, u64, vp, vp, vp, vp, vp])
+        _sig(lib, "zp_probe_tiles_codes_device", i32, [vp, u64, u64, vp, vp, vp, vp, vp])
         _sig(lib, "zp_gen_lengths_device", i32, [i32, u64, u64, u64, vp, vp])
         _sig(lib, "zp_gen_frames_device", i32, [i32, u64, u64, u64, vp, vp, vp, vp])
         _sig(lib, "zp_reader_new", i32, [i32, vp, u64, vp])

@@ -55,6 +55,7 @@
 // tools/build_variants.sh (tools/kbench.py --variants); this file is the
 // product kernel only.
 
+#ifndef ZP_PARSE_SLOTS_TU
 static __thread char g_last_error[256];
 
 static void set_err(const char* what, hipError_t e) {
@@ -65,6 +66,7 @@ extern "C" const char* zp_last_error(void) { return g_last_error; }
 extern "C" __attribute__((visibility("hidden"))) char* zp__errbuf(void) { return g_last_error; }
 extern "C" int zp_abi_version(void) { return ZP_ABI_VERSION; }
 extern "C" const char* zp_err_str(int code) { return zp_err_string(code); }
+#endif
 
 // --------------------------------------------------------------------------
 // Device helpers
@@ -716,8 +718,45 @@ __device__ __forceinline__ uint32_t tiny_be16(const uint32_t (&f)[16], uint32_t 
     const uint32_t d = f[x >> 2] >> (8 * (x & 2));                 // x even
     return ((d & 0xFFu) << 8) | ((d >> 8) & 0xFFu);
 }
+// Record codes (round 6). Inside the read stream a record store costs the
+// stream in proportion to the contiguous bytes a wave stores: 64 x 8 B
+// +0.23 ms on c3, 64 B per tile +0.044 (DESIGN.md §4,
+// profiles/r06_rec_slot_probe.log). A full tile whose 64 records all have
+// the common form (no error, no IP-in-IP, no extension headers, Ethernet
+// code 0-2, the L4 reader right after a 20-B IPv4 or 40-B IPv6 header)
+// stores one byte per frame over its first 8 records instead, and
+// zp_rec_expand_kernel rewrites the tile's 64 records from them after the
+// parse (write-only, ~0.03 ms on c3). Code = 0xC0 + 15 * eth_code + 5 * l3
+// + l4 (l3: ARP / IPv4 / IPv6, l4: none / TCP / UDP / ICMPv4 / ICMPv6):
+// byte 3 of a tile's first record is <= 0x97 (err <= 37), of a code tile
+// >= 0xC0. Any other tile (a record without a code, a partial last tile,
+// the fused column kernel, the zp_parse_one server) stores its records.
+#define ZP_CODE_BASE 0xC0u
+__device__ __forceinline__ uint32_t rec_code(zp_u32x2 pk) {
+    const uint32_t f = pk.x, ec = (f >> 24) & 3u;
+    const uint32_t l3 = (f & ZP_F_ARP) ? 0u : (f & ZP_F_IPV4) ? 1u : (f & ZP_F_IPV6) ? 2u : 3u;
+    const uint32_t l4 = (f & ZP_F_TCP) ? 1u : (f & ZP_F_UDP) ? 2u : (f & ZP_F_ICMPV4) ? 3u
+                      : (f & ZP_F_ICMPV6) ? 4u : 0u;
+    const uint32_t want = ZP_F_ETHERNET | (l3 == 0 ? ZP_F_ARP : l3 == 1 ? ZP_F_IPV4 : ZP_F_IPV6) |
+                          (l4 == 1 ? ZP_F_TCP : l4 == 2 ? ZP_F_UDP : l4 == 3 ? ZP_F_ICMPV4
+                           : l4 == 4 ? ZP_F_ICMPV6 : 0u);
+    const uint32_t off = l4 ? 14u + 4u * ec + (l3 == 1 ? 20u : 40u) : 0u;
+    const bool ok = ec < 3u && l3 < 3u && (l3 != 0 || l4 == 0) && (f & 0xFCFFFFFFu) == want &&
+                    pk.y == off;
+    return ok ? ZP_CODE_BASE + 15u * ec + 5u * l3 + l4 : 0u;
+}
+// The record of a code (zp_rec_expand_kernel).
+__device__ __forceinline__ zp_u32x2 code_rec(uint32_t c) {
+    const uint32_t x = c - ZP_CODE_BASE, ec = x / 15u, l3 = x / 5u % 3u, l4 = x % 5u;
+    const uint32_t f = ZP_F_ETHERNET | (l3 == 0 ? ZP_F_ARP : l3 == 1 ? ZP_F_IPV4 : ZP_F_IPV6) |
+                       (l4 == 1 ? ZP_F_TCP : l4 == 2 ? ZP_F_UDP : l4 == 3 ? ZP_F_ICMPV4
+                        : l4 == 4 ? ZP_F_ICMPV6 : 0u) | ec << 24;
+    return zp_u32x2{f, l4 ? 14u + 4u * ec + (l3 == 1 ? 20u : 40u) : 0u};
+}
+
+
 __device__ __forceinline__ bool tiny_tile(uint64_t tile, uint32_t len, uintptr_t ga, uint64_t n,
-                                          int lane, zp_record* __restrict__ records) {
+                                          int lane, zp_record* __restrict__ records, bool slots) {
     const bool live = tile * 64 + lane < n;
     const uintptr_t base = ga & ~(uintptr_t)3;
     const uint32_t sh = (uint32_t)(ga & 3);
@@ -751,6 +790,11 @@ __device__ __forceinline__ bool tiny_tile(uint64_t tile, uint32_t len, uintptr_t
     for (int k = 9; k < 16; ++k) lv = sad16(f[k], lv);
     ok = ok && csum_ok(acc, lv, false);
     if (__ballot(live && !ok)) return false;                           // wave-uniform
+    if (slots && tile * 64 + 64 <= n) {                               // every lane live: codes
+        const uint32_t c = ZP_CODE_BASE + 5u + (tcp ? 1u : udp ? 2u : 3u);   // code 0, IPv4
+        __builtin_nontemporal_store((uint8_t)c, (uint8_t*)(records + tile * 64) + lane);
+        return true;
+    }
     if (live) {
         // Ethernet II (code 0), IPv4, the L4 reader at 34
         const uint32_t flags = ZP_F_ETHERNET | ZP_F_IPV4 | (tcp ? ZP_F_TCP : udp ? ZP_F_UDP : ZP_F_ICMPV4);
@@ -765,7 +809,7 @@ __device__ __forceinline__ void store_ext(zp_ext_offsets* base, uint64_t i, uint
 
 // Header walk + checksum verdict + record store of a streamed tile; with COLS
 // also the column views, from the same LDS window (no second pass).
-template <bool COLS, bool SYS = false, class L = WaveLds>
+template <bool COLS, bool SYS = false, class L = WaveLds, bool SLOTS = false>
 __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, L& lds,
                                             zp_record* __restrict__ records,
                                             zp_ext_offsets* __restrict__ ext,
@@ -845,13 +889,18 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
     // L4 sum = that - V[A & ~15, A + l4) - V[E, E16).
     zp_rec_full rec = w.rec;
     const uint64_t p = s.tile * 64 + lane;
-    // The record as the walk left it goes out before the verdict, so its
-    // store's latency overlaps the checksum work instead of ending the wave
-    // (two boxes: c5 -1.6 / -0.6 %, c3 -0.3 / +0.6 %, c4 -0.4 / +0.3 %;
-    // profiles/r05_kbench_early_rec.log, r05_kbench_early_rec_k2_norec.log);
-    // a frame whose L4 checksum then fails stores its error record over it
-    // (same lane, same address: the later store lands last).
-    if (!SYS) __builtin_nontemporal_store(zp_pack(rec), (zp_u32x2*)(records + p));
+    // A full tile whose walk records all have codes stores after the verdict
+    // (wave-uniform: all 64 lanes are live only in a full tile).
+    const bool slot = SLOTS && !SYS && !COLS && __ballot(true) == ~0ull &&
+                      !__ballot(rec_code(zp_pack(rec)) == 0u);
+    // Otherwise the record as the walk left it goes out before the verdict,
+    // so its store's latency overlaps the checksum work instead of ending
+    // the wave (two boxes: c5 -1.6 / -0.6 %, c3 -0.3 / +0.6 %, c4 -0.4 /
+    // +0.3 %; profiles/r05_kbench_early_rec.log,
+    // r05_kbench_early_rec_k2_norec.log); a frame whose L4 checksum then
+    // fails stores its error record over it (same lane, same address: the
+    // later store lands last).
+    if (!SYS && !slot) __builtin_nontemporal_store(zp_pack(rec), (zp_u32x2*)(records + p));
     if (w.pending) {
         bool ok;
         if (s.giant) {
@@ -865,25 +914,25 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
         if (!ok) {
             rec = zp_rec_full{};
             rec.err = (uint8_t)(w.v6 ? ZP_ERR_IPV6_L4_CHECKSUM : ZP_ERR_IPV4_L4_CHECKSUM);
-            if (!SYS) __builtin_nontemporal_store(zp_pack(rec), (zp_u32x2*)(records + p));
+            if (!SYS && !slot) __builtin_nontemporal_store(zp_pack(rec), (zp_u32x2*)(records + p));
         }
     }
+    // Records are nontemporal 8-B stores, one per frame (512 B of whole
+    // lines per wave instruction): nt took 6-7 % off on every placement,
+    // 16-B records (v2) 4-6 % against 32-B ones, 8-B records (v4) 2-7 % more.
     static_assert(sizeof(zp_record) == 8 && sizeof(zp_ext_offsets) == 16, "8-B records");
-    if (SYS)
-    {
-        // One nontemporal 8-B store per frame: 512 B of whole lines per wave
-        // instruction. Writes mixed into the read stream cost several times
-        // their bytes and make the kernel sensitive to the placement of the
-        // arena and the records: nt took 6-7 % off on every
-        // placement, 16-B records (v2) 4-6 % against 32-B ones, and 8-B
-        // records (v4) 2-7 % more.
-        if (SYS) {
-            // the server stores it with its acknowledgement (one 16-B store)
-            *sys_rec = zp_pack(rec);
-        } else {
-            __builtin_nontemporal_store(zp_pack(rec), (zp_u32x2*)(records + p));
-        }
+    if (slot) {
+        // the final records (a failed checksum has no code): codes if every
+        // frame still has one, else every lane's record
+        const zp_u32x2 pk = zp_pack(rec);
+        const uint32_t c = rec_code(pk);
+        if (!__ballot(c == 0u))
+            __builtin_nontemporal_store((uint8_t)c, (uint8_t*)(records + s.tile * 64) + lane);
+        else
+            __builtin_nontemporal_store(pk, (zp_u32x2*)(records + p));
     }
+    // the server stores it with its acknowledgement (one 16-B store)
+    if (SYS) *sys_rec = zp_pack(rec);
     if (ext) {
         // The extension chains: a wave with at least ZP_EXT_DENSE chains
         // writes the entries of all its frames (whole lines, zero where
@@ -928,7 +977,7 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
 #define ZP_KATTR_COLS __launch_bounds__(64 * ZP_WAVES)
 // One streamed tile: descriptors given (len, ga), stream, walk, verdict,
 // record store (the batch kernels).
-template <bool COLS, bool TINY = !COLS, class L = WaveLds>
+template <bool COLS, bool TINY = !COLS, class L = WaveLds, bool SLOTS = false>
 __device__ __forceinline__ void parse_tile(uint64_t t, uint32_t len, uintptr_t ga, uint64_t n,
                                            int lane, L& lds,
                                            zp_record* __restrict__ records,
@@ -939,7 +988,7 @@ __device__ __forceinline__ void parse_tile(uint64_t t, uint32_t len, uintptr_t g
     uint4* tail = &lds.win[0] + ZP_WIN_CH * 64;
     // a tile of 64-B frames: registers only (wave-uniform test)
     if (TINY && !__ballot(t * 64 + lane < n && len != 64u) &&
-        tiny_tile(t, len, ga, n, lane, records))
+        tiny_tile(t, len, ga, n, lane, records, SLOTS))
         return;
     TileState s;
     tile_setup(s, t, len, ga, n, lane, lds);
@@ -992,10 +1041,10 @@ __device__ __forceinline__ void parse_tile(uint64_t t, uint32_t len, uintptr_t g
         s.ga = org + 16ull * bperm(s.R.pfx, r) + s.shift;
     }
     __builtin_amdgcn_s_setprio(0);             // walk at priority 0 ...
-    tile_finish<COLS, false, L>(s, n, lane, lds, records, ext, cols);
+    tile_finish<COLS, false, L, SLOTS>(s, n, lane, lds, records, ext, cols);
 }
 
-template <bool COLS>
+template <bool COLS, bool SLOTS = false>
 __device__ __forceinline__ void parse_tiles(const uint8_t* __restrict__ arena,
                                             const uint64_t* __restrict__ offs,
                                             const uint32_t* __restrict__ lens, uint64_t n,
@@ -1018,16 +1067,85 @@ __device__ __forceinline__ void parse_tiles(const uint8_t* __restrict__ arena,
         uint32_t len;
         uintptr_t ga;
         load_desc(arena, offs, lens, n, t, lane, len, ga);
-        parse_tile<COLS>(t, len, ga, n, lane, lds, records, ext, cols);
+        parse_tile<COLS, !COLS, WaveLds, SLOTS>(t, len, ga, n, lane, lds, records, ext, cols);
     }
 }
 
+#ifdef ZP_PARSE_SLOTS_TU
+// The parse kernel with record slots, alone in its translation unit
+// (zp_parse_slots.hip): compiled beside zp_parse_kernel in one module, the
+// second instantiation of the tile code changed zp_parse_kernel's register
+// allocation (2 VGPRs spilled, SGPRs 94 -> 98).
+__global__ void ZP_KATTR
+zp_parse_slots_kernel(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs,
+                      const uint32_t* __restrict__ lens, uint64_t n,
+                      zp_record* __restrict__ records, zp_ext_offsets* __restrict__ ext) {
+    const ColPtrs none{};
+    parse_tiles<false, true>(arena, offs, lens, n, records, ext, none);
+}
+extern "C" __attribute__((visibility("hidden"))) hipError_t
+zp__parse_slots_launch(uint64_t blocks, hipStream_t stream, const uint8_t* arena, const uint64_t* offs,
+                       const uint32_t* lens, uint64_t n, zp_record* records, zp_ext_offsets* ext) {
+    hipLaunchKernelGGL(zp_parse_slots_kernel, dim3((unsigned)blocks), dim3(64 * ZP_WAVES), 0, stream,
+                       arena, offs, lens, n, records, ext);
+    return hipGetLastError();
+}
+#else
+extern "C" hipError_t zp__parse_slots_launch(uint64_t blocks, hipStream_t stream, const uint8_t* arena,
+                                             const uint64_t* offs, const uint32_t* lens, uint64_t n,
+                                             zp_record* records, zp_ext_offsets* ext);
 __global__ void ZP_KATTR
 zp_parse_kernel(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ offs,
                 const uint32_t* __restrict__ lens, uint64_t n,
                 zp_record* __restrict__ records, zp_ext_offsets* __restrict__ ext) {
     const ColPtrs none{};
     parse_tiles<false>(arena, offs, lens, n, records, ext, none);
+}
+
+// The records of every code tile from its codes (after the parse kernel on
+// the same stream): a wave takes ZP_EXPAND_TILES tiles, finds the code tiles
+// among them from one byte each, and lane l rewrites record l of each from
+// code l; a tile whose first bytes are a record is left as the parse stored
+// it. Only full tiles can hold codes.
+#define ZP_EXPAND_TILES 16    // tiles per wave: one load finds the code tiles among them
+__global__ void __launch_bounds__(256) zp_rec_expand_kernel(zp_record* __restrict__ records, uint64_t n) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t t0 = ((uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * ZP_EXPAND_TILES;
+    const uint64_t full = n / 64;                       // tiles that can hold codes
+    // byte 3 of each tile (lanes 0-15): >= ZP_CODE_BASE marks a code tile
+    const uint32_t b3 = lane < ZP_EXPAND_TILES && t0 + lane < full
+                            ? ((const uint8_t*)(records + (t0 + lane) * 64))[3] : 0u;
+    const uint64_t m = __ballot(b3 >= ZP_CODE_BASE);
+    if (!m) return;
+    uint32_t c[ZP_EXPAND_TILES];
+#pragma unroll
+    for (int k = 0; k < ZP_EXPAND_TILES; ++k)           // the codes, all loads in flight
+        c[k] = (m >> k) & 1u ? ((const uint8_t*)(records + (t0 + k) * 64))[lane] : 0u;
+#pragma unroll
+    for (int k = 0; k < ZP_EXPAND_TILES; ++k)
+        if ((m >> k) & 1u)
+            __builtin_nontemporal_store(code_rec(c[k]), (zp_u32x2*)(records + (t0 + k) * 64 + lane));
+}
+
+extern "C" __attribute__((visibility("hidden"))) int zp__rec_expand_launch(zp_record* records, uint64_t n,
+                                                                         hipStream_t stream) {
+    if (n < 64) return 0;
+    const uint64_t per_block = 4 * ZP_EXPAND_TILES;              // tiles
+    hipLaunchKernelGGL(zp_rec_expand_kernel, dim3((unsigned)((n / 64 + per_block - 1) / per_block)),
+                       dim3(256), 0, stream, records, n);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) { set_err("zp_rec_expand_kernel launch", e); return -2; }
+    return 0;
+}
+
+// Record codes (0 auto: batches of at least ZP_SLOT_MIN_FRAMES, 1 always,
+// 2 never): zp_set_record_slots. Below that the second launch costs more
+// than the codes save (c2, 1M x 64 B).
+#define ZP_SLOT_MIN_FRAMES (1ull << 21)
+static int g_slot_mode = 0;
+extern "C" int zp_set_record_slots(int mode) {
+    if (mode < 0 || mode > 2) return -1;
+    return __atomic_exchange_n(&g_slot_mode, mode, __ATOMIC_RELAXED);
 }
 
 // Parse + column views in one pass (zp_parse_batch_columns_device).
@@ -1054,11 +1172,18 @@ extern "C" int zp_parse_batch_device(const uint8_t* arena, const uint64_t* offs,
         snprintf(g_last_error, sizeof g_last_error, "zp_parse_batch_device: batch too large");
         return -1;
     }
-    hipLaunchKernelGGL(zp_parse_kernel, dim3((unsigned)blocks), dim3(64 * ZP_WAVES), 0,
-                       (hipStream_t)stream, arena, offs, lens, n, records, ext);
-    const hipError_t e = hipGetLastError();
+    const int mode = __atomic_load_n(&g_slot_mode, __ATOMIC_RELAXED);
+    const int slots = mode == 1 || (mode == 0 && n >= ZP_SLOT_MIN_FRAMES);
+    hipError_t e;
+    if (slots) {
+        e = zp__parse_slots_launch(blocks, (hipStream_t)stream, arena, offs, lens, n, records, ext);
+    } else {
+        hipLaunchKernelGGL(zp_parse_kernel, dim3((unsigned)blocks), dim3(64 * ZP_WAVES), 0,
+                           (hipStream_t)stream, arena, offs, lens, n, records, ext);
+        e = hipGetLastError();
+    }
     if (e != hipSuccess) { set_err("zp_parse_kernel launch", e); return -2; }
-    return 0;
+    return slots ? zp__rec_expand_launch(records, n, (hipStream_t)stream) : 0;
 }
 
 extern "C" int zp_parse_batch_columns_device(const uint8_t* arena, const uint64_t* offs,
@@ -1276,3 +1401,4 @@ extern "C" __attribute__((visibility("hidden"))) int zp__one_stall_launch(uint64
     if (e != hipSuccess) { set_err("zp_one_stall_kernel launch", e); return -2; }
     return 0;
 }
+#endif  // ZP_PARSE_SLOTS_TU

@@ -204,6 +204,7 @@ extern "C" int zp_probe_read_device(const uint8_t* p, uint64_t bytes, uint32_t* 
 // --------------------------------------------------------------------------
 #define PT_LDS_BYTES 8960          // sizeof(WaveLds) of the parse kernel (ZP_WIN 112)
 
+template <bool CODES>
 __global__ void __launch_bounds__(64) zp_probe_tiles_kernel(const uint8_t* __restrict__ p,
                                                             uint64_t nchunks, uint64_t cpt,
                                                             uint64_t n,
@@ -236,7 +237,10 @@ __global__ void __launch_bounds__(64) zp_probe_tiles_kernel(const uint8_t* __res
     pad[lane] = acc;                         // the LDS allocation stays (occupancy)
     __builtin_amdgcn_wave_barrier();
     acc ^= pad[lane ^ 1];
-    if (records) {
+    if (CODES && 64 * t + 64 <= n) {         // a full tile: one code byte per frame
+        __builtin_nontemporal_store((uint8_t)(0xC5u + (acc == 0x9E3779B9u)),
+                                    (uint8_t*)(records + 64 * t) + lane);
+    } else if (records) {
         if (64 * t + lane < n)
             __builtin_nontemporal_store(((uint64_t)acc << 32) | (uint32_t)t, records + 64 * t + lane);
     } else if (acc == 0x9E3779B9u) {
@@ -259,7 +263,7 @@ extern "C" int zp_probe_tiles_device(const uint8_t* p, uint64_t bytes, uint64_t 
     }
     const uint64_t nchunks = bytes / 16;
     const uint64_t cpt = (nchunks + tiles - 1) / tiles;
-    hipLaunchKernelGGL(zp_probe_tiles_kernel, dim3((unsigned)tiles), dim3(64), 0,
+    hipLaunchKernelGGL(zp_probe_tiles_kernel<false>, dim3((unsigned)tiles), dim3(64), 0,
                        (hipStream_t)stream, p, nchunks, cpt, n, offs, lens, (uint64_t*)records,
                        sink);
     const hipError_t e = hipGetLastError();
@@ -268,4 +272,34 @@ extern "C" int zp_probe_tiles_device(const uint8_t* p, uint64_t bytes, uint64_t 
         return -2;
     }
     return 0;
+}
+
+// The same pattern with record codes (zp_set_record_slots): a full tile
+// stores one byte per frame (a valid code) instead of its 8-B records, and
+// the parse's expansion kernel rewrites the records after it.
+extern "C" int zp__rec_expand_launch(zp_record* records, uint64_t n, hipStream_t stream);
+extern "C" int zp_probe_tiles_codes_device(const uint8_t* p, uint64_t bytes, uint64_t n,
+                                           const uint64_t* offs, const uint32_t* lens,
+                                           zp_record* records, uint32_t* sink, void* stream) {
+    if (!p || !sink || !records || ((uintptr_t)p & 15) || ((uintptr_t)records & 7)) {
+        snprintf(zp__errbuf(), 256, "zp_probe_tiles_codes_device: null or unaligned pointer");
+        return -1;
+    }
+    const uint64_t tiles = (n + 63) / 64;
+    if (bytes < 16 || tiles == 0) return 0;
+    if (tiles > 0x7FFFFFFFull) {
+        snprintf(zp__errbuf(), 256, "zp_probe_tiles_codes_device: too many tiles");
+        return -1;
+    }
+    const uint64_t nchunks = bytes / 16;
+    const uint64_t cpt = (nchunks + tiles - 1) / tiles;
+    hipLaunchKernelGGL(zp_probe_tiles_kernel<true>, dim3((unsigned)tiles), dim3(64), 0,
+                       (hipStream_t)stream, p, nchunks, cpt, n, offs, lens, (uint64_t*)records,
+                       sink);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        snprintf(zp__errbuf(), 256, "zp_probe_tiles_kernel launch: %s", hipGetErrorString(e));
+        return -2;
+    }
+    return zp__rec_expand_launch(records, n, (hipStream_t)stream);
 }
