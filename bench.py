@@ -455,7 +455,8 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "traffic_source": traffic_src,
-                     "kernel": "zp_parse_kernel",
+                     "kernel": ("zp_parse_slots_kernel + zp_rec_expand_kernel (record codes)"
+                                if zp.batch.record_codes(n) else "zp_parse_kernel"),
                      "kernel_ms_mean": round(kmean, 4), "kernel_ms_min": round(min(kms), 4),
                      "algorithmic_bytes_per_launch": total_bytes},
     }

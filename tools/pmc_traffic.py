@@ -1,5 +1,7 @@
 """Turns a rocprofv3 --pmc TCC_EA0_RDREQ_sum/TCC_EA0_WRREQ_sum pass over
-bench.py into per-launch HBM bytes of zp_parse_kernel.
+bench.py into per-launch HBM bytes of the parse: zp_parse_kernel, or with
+record codes (zp_set_record_slots, from 2M frames) zp_parse_slots_kernel +
+zp_rec_expand_kernel (one of each per launch).
 
 gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE is
 TCC_EA0_RDREQ x 64 B and reports exactly half of the bytes of a wide
@@ -19,12 +21,18 @@ def main():
     d, cfg, out = sys.argv[1], sys.argv[2], sys.argv[3]
     paths = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     s = summarize(paths)
-    rd = s[("zp_parse_kernel", "TCC_EA0_RDREQ_sum")]
-    wr = s[("zp_parse_kernel", "TCC_EA0_WRREQ_sum")]
+    names = [k for k in ("zp_parse_kernel", "zp_parse_slots_kernel", "zp_rec_expand_kernel")
+             if (k, "TCC_EA0_RDREQ_sum") in s]
+    per = {k: {"RDREQ": s[(k, "TCC_EA0_RDREQ_sum")][0], "WRREQ": s[(k, "TCC_EA0_WRREQ_sum")][0],
+               "dispatches": s[(k, "TCC_EA0_RDREQ_sum")][1]} for k in names}
+    main_k = "zp_parse_slots_kernel" if "zp_parse_slots_kernel" in per else "zp_parse_kernel"
+    launch = [main_k] + (["zp_rec_expand_kernel"] if main_k == "zp_parse_slots_kernel" else [])
+    rd = (sum(per[k]["RDREQ"] for k in launch), per[main_k]["dispatches"])
+    wr = (sum(per[k]["WRREQ"] for k in launch), per[main_k]["dispatches"])
     bench = [l for l in open(os.path.join(d, "bench.log")) if l.startswith("{")]
     b = json.loads(bench[-1]) if bench else {}
     res = {
-        "kernel": "zp_parse_kernel", "config": cfg,
+        "kernel": " + ".join(launch), "config": cfg, "per_kernel": per,
         "frames_per_launch": b.get("config", {}).get("frames_per_gpu"),
         "algorithmic_bytes_per_launch": b.get("roofline", {}).get("algorithmic_bytes_per_launch"),
         "dispatches": rd[1],

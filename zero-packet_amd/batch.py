@@ -26,6 +26,18 @@ from . import _lib
 from .records import EXT_BYTES, EXT_DTYPE, RECORD_BYTES, RECORD_DTYPE, expand_ext
 
 CONFIGS = {"c1": 1, "c2": 2, "c3": 3, "c4": 4, "c5": 5, "c6": 6}
+# zp_set_record_slots' automatic mode stores record codes from this many
+# frames on (ZP_SLOT_MIN_FRAMES, zp_parse.hip)
+RECORD_CODES_MIN_FRAMES = 1 << 21
+
+
+def record_codes(n):
+    """Whether a parse of n frames takes the record-code kernels under the
+    process' zp_set_record_slots mode (0 auto, 1 always, 2 never)."""
+    lib = _lib.hip()
+    mode = lib.zp_set_record_slots(0)
+    lib.zp_set_record_slots(mode)
+    return mode == 1 or (mode == 0 and n >= RECORD_CODES_MIN_FRAMES)
 SEED = 0x5EED2025
 
 
