@@ -152,3 +152,28 @@ def test_slots_auto_mode_full_size(zp, slots, cfg):
         got[mode] = r
     assert torch.equal(got[0], got[2])
     assert int((zp.batch.record_err(got[0]) != 0).sum()) == 0
+
+
+@pytest.mark.gpu
+def test_slots_mixed_tiles(zp, slots):
+    """Config-5 tiles (IP-in-IP and VLAN tags: records) and config-3 tiles
+    (codes) side by side in one batch, with one frame's L4 checksum failing
+    in every third tile (those tiles store records after the verdict)."""
+    a5, o5, l5 = zp.batch.generate_host("c5", 64 * 150, first=123)
+    a3, o3, l3 = zp.batch.generate_host("c3", 64 * 150, first=456)
+    frames = []
+    for t in range(150):
+        for a, o, l_ in ((a5, o5, l5), (a3, o3, l3)):
+            frames += [bytearray(a[int(o[i]):int(o[i]) + int(l_[i])]) for i in range(64 * t, 64 * t + 64)]
+    for t in range(0, 300, 3):
+        f = frames[64 * t + 17]
+        f[-1] ^= 1
+    lens = np.array([len(f) for f in frames], np.uint32)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1].astype(np.int64))]).astype(np.int64)
+    arena = np.zeros(int(offs[-1] + lens[-1]) + 64, np.uint8)
+    for o, f in zip(offs, frames):
+        arena[o:o + len(f)] = np.frombuffer(bytes(f), np.uint8)
+    out = parse_modes(zp, slots, arena, offs, lens)
+    want = check(zp, out, arena, offs, lens)
+    inner = (want["flags"] & zp.records.F_IP_IN_IP) != 0
+    assert inner.sum() > 1000 and (want["err"] != 0).sum() == 100
