@@ -312,9 +312,12 @@ int zp_parse_batch_device(const uint8_t* arena, const uint64_t* offs,
  * frame over the tile's first 8 records, and a second kernel on the same
  * stream rewrites the tile's 64 records from the codes. The records a
  * caller reads are the same either way (zp_parse_batch_device still only
- * enqueues). mode 0: automatic (batches of at least 2,097,152 frames),
- * 1: always, 2: never. Process-wide; returns the previous mode, or -1 for
- * an unknown mode.
+ * enqueues). mode 0: automatic (batches of at least 2,097,152 frames
+ * whose traffic has code tiles: probe calls, one per 16 calls per device
+ * and one at every change of batch size, tell, through a mapped host word
+ * their second kernel sets and an event queried without waiting), 1:
+ * always, 2: never. Process-wide; returns the previous mode, or -1 for an
+ * unknown mode.
  */
 int zp_set_record_slots(int mode);
 

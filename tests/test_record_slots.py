@@ -139,19 +139,29 @@ def test_slots_min_size_tiles(zp, slots):
 @pytest.mark.gpu
 @pytest.mark.parametrize("cfg", ["c3", "c5"])
 def test_slots_auto_mode_full_size(zp, slots, cfg):
-    """The automatic mode takes codes from 2,097,152 frames on: 4M frames
-    parse to the same bytes with codes (auto) and without (never)."""
+    """The automatic mode takes codes from 2,097,152 frames on, learning
+    from probe calls whether the traffic has code tiles (c3: yes, c5: no):
+    40 calls on 4M frames, back to back and with synchronisations between
+    them (probes completing or not), each parse to the same bytes as the
+    code-free path."""
     n = 4 << 20
     arena, offs, lens = zp.batch.generate(cfg, n, device=dev())
-    got = {}
-    for mode in (0, 2):
-        slots(mode)
-        rec = torch.full((n, 8), 0xFF, dtype=torch.uint8, device=arena.device)
-        r, _ = zp.batch.parse_batch(arena, offs, lens, rec, check=False)
-        torch.cuda.synchronize()
-        got[mode] = r
-    assert torch.equal(got[0], got[2])
-    assert int((zp.batch.record_err(got[0]) != 0).sum()) == 0
+    slots(2)
+    want = torch.full((n, 8), 0xFF, dtype=torch.uint8, device=arena.device)
+    zp.batch.parse_batch(arena, offs, lens, want, check=False)
+    slots(0)
+    recs = [torch.full((n, 8), 0xA5, dtype=torch.uint8, device=arena.device) for _ in range(4)]
+    for k in range(40):
+        r = recs[k % 4]
+        r.fill_(0xA5 if k % 2 else 0xFF)
+        zp.batch.parse_batch(arena, offs, lens, r, check=False)
+        if k % 3 == 0:
+            torch.cuda.synchronize()
+        if k % 4 == 3:
+            torch.cuda.synchronize()
+            for q in recs:
+                assert torch.equal(q, want)
+    assert int((zp.batch.record_err(want) != 0).sum()) == 0
 
 
 @pytest.mark.gpu

@@ -33,6 +33,7 @@
 #include <string.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <mutex>
 
 #include "../../include/zero_packet.h"
 #include "../../include/zero_packet_errstr.h"
@@ -891,7 +892,10 @@ __device__ __forceinline__ void tile_finish(TileState& s, uint64_t n, int lane, 
     const uint64_t p = s.tile * 64 + lane;
     // A full tile whose walk records all have codes stores after the verdict
     // (wave-uniform: all 64 lanes are live only in a full tile).
+    // (a flags test first: a tile with an error, a tunnel or a chain skips
+    // the code arithmetic)
     const bool slot = SLOTS && !SYS && !COLS && __ballot(true) == ~0ull &&
+                      !__ballot((zp_pack(rec).x & (0xFC000000u | ZP_F_IP_IN_IP | ZP_F_EXT | ZP_F_INNER_EXT)) != 0u) &&
                       !__ballot(rec_code(zp_pack(rec)) == 0u);
     // Otherwise the record as the walk left it goes out before the verdict,
     // so its store's latency overlaps the checksum work instead of ending
@@ -1108,7 +1112,8 @@ zp_parse_kernel(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ 
 // code l; a tile whose first bytes are a record is left as the parse stored
 // it. Only full tiles can hold codes.
 #define ZP_EXPAND_TILES 16    // tiles per wave: one load finds the code tiles among them
-__global__ void __launch_bounds__(256) zp_rec_expand_kernel(zp_record* __restrict__ records, uint64_t n) {
+__global__ void __launch_bounds__(256) zp_rec_expand_kernel(zp_record* __restrict__ records, uint64_t n,
+                                                             uint32_t* __restrict__ hint, uint32_t token) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t t0 = ((uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * ZP_EXPAND_TILES;
     const uint64_t full = n / 64;                       // tiles that can hold codes
@@ -1117,6 +1122,10 @@ __global__ void __launch_bounds__(256) zp_rec_expand_kernel(zp_record* __restric
                             ? ((const uint8_t*)(records + (t0 + lane) * 64))[3] : 0u;
     const uint64_t m = __ballot(b3 >= ZP_CODE_BASE);
     if (!m) return;
+    // (a probe of the automatic mode: every 64th workgroup that finds code
+    // tiles says so, in mapped host memory)
+    if (hint && lane == 0 && (threadIdx.x >> 6) == 0 && (blockIdx.x & 63u) == 0)
+        __hip_atomic_store(hint, token, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     uint32_t c[ZP_EXPAND_TILES];
 #pragma unroll
     for (int k = 0; k < ZP_EXPAND_TILES; ++k)           // the codes, all loads in flight
@@ -1128,11 +1137,12 @@ __global__ void __launch_bounds__(256) zp_rec_expand_kernel(zp_record* __restric
 }
 
 extern "C" __attribute__((visibility("hidden"))) int zp__rec_expand_launch(zp_record* records, uint64_t n,
-                                                                         hipStream_t stream) {
+                                                                         hipStream_t stream,
+                                                                         uint32_t* hint, uint32_t token) {
     if (n < 64) return 0;
     const uint64_t per_block = 4 * ZP_EXPAND_TILES;              // tiles
     hipLaunchKernelGGL(zp_rec_expand_kernel, dim3((unsigned)((n / 64 + per_block - 1) / per_block)),
-                       dim3(256), 0, stream, records, n);
+                       dim3(256), 0, stream, records, n, hint, token);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) { set_err("zp_rec_expand_kernel launch", e); return -2; }
     return 0;
@@ -1146,6 +1156,43 @@ static int g_slot_mode = 0;
 extern "C" int zp_set_record_slots(int mode) {
     if (mode < 0 || mode > 2) return -1;
     return __atomic_exchange_n(&g_slot_mode, mode, __ATOMIC_RELAXED);
+}
+
+// The automatic mode learns per device whether the traffic has code tiles:
+// the first automatic call and every ZP_SLOT_PROBE_EVERY-th one after its
+// predecessor's result is known run the code kernels with a mapped host
+// word the expansion sets when it finds code tiles; once that call has
+// completed (an event, queried without waiting) the following calls take
+// the code kernels only if it found some. Traffic without code tiles (c5,
+// c4) then runs zp_parse_kernel alone but for the probes. Under stream
+// capture the last decision is used as is; a call with another batch size
+// than the last probes at once. A hint only: either kernel writes the same
+// records.
+#define ZP_SLOT_PROBE_EVERY 16
+struct SlotState {
+    std::mutex mu;
+    uint32_t* word = nullptr;          // mapped host word (host view)
+    uint32_t* word_d = nullptr;        // its device view
+    hipEvent_t ev = nullptr;
+    bool pending = false, decision = true, broken = false;
+    uint64_t since = 0;                // automatic calls since the last probe
+    uint64_t last_n = 0;               // a new batch size probes at once
+    uint32_t token = 0;                // the pending probe's (the word holds the last finder's)
+};
+static SlotState g_slot_state[64];
+
+static bool slot_state_init(SlotState& st) {
+    if (st.word || st.broken) return !st.broken;
+    void* w = nullptr;
+    if (hipHostMalloc(&w, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer((void**)&st.word_d, w, 0) != hipSuccess ||
+        hipEventCreateWithFlags(&st.ev, hipEventDisableTiming) != hipSuccess) {
+        (void)hipGetLastError();
+        st.broken = true;                                    // decide without probes
+        return false;
+    }
+    st.word = (uint32_t*)w;
+    return true;
 }
 
 // Parse + column views in one pass (zp_parse_batch_columns_device).
@@ -1173,17 +1220,50 @@ extern "C" int zp_parse_batch_device(const uint8_t* arena, const uint64_t* offs,
         return -1;
     }
     const int mode = __atomic_load_n(&g_slot_mode, __ATOMIC_RELAXED);
-    const int slots = mode == 1 || (mode == 0 && n >= ZP_SLOT_MIN_FRAMES);
-    hipError_t e;
-    if (slots) {
-        e = zp__parse_slots_launch(blocks, (hipStream_t)stream, arena, offs, lens, n, records, ext);
-    } else {
-        hipLaunchKernelGGL(zp_parse_kernel, dim3((unsigned)blocks), dim3(64 * ZP_WAVES), 0,
-                           (hipStream_t)stream, arena, offs, lens, n, records, ext);
-        e = hipGetLastError();
+    const hipStream_t st_h = (hipStream_t)stream;
+    auto launch = [&](bool slots, uint32_t* hint, uint32_t token) -> int {
+        hipError_t e;
+        if (slots) {
+            e = zp__parse_slots_launch(blocks, st_h, arena, offs, lens, n, records, ext);
+        } else {
+            hipLaunchKernelGGL(zp_parse_kernel, dim3((unsigned)blocks), dim3(64 * ZP_WAVES), 0,
+                               st_h, arena, offs, lens, n, records, ext);
+            e = hipGetLastError();
+        }
+        if (e != hipSuccess) { set_err("zp_parse_kernel launch", e); return -2; }
+        return slots ? zp__rec_expand_launch(records, n, st_h, hint, token) : 0;
+    };
+    if (mode != 0 || n < ZP_SLOT_MIN_FRAMES) return launch(mode == 1, nullptr, 0);
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) { (void)hipGetLastError(); dev = 0; }
+    SlotState& st = g_slot_state[dev & 63];
+    std::lock_guard<std::mutex> guard(st.mu);
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st_h, &cs) != hipSuccess) { (void)hipGetLastError(); cs = hipStreamCaptureStatusActive; }
+    if (cs != hipStreamCaptureStatusNone) return launch(st.decision, nullptr, 0);
+    if (n != st.last_n) {                       // another workload: probe now
+        st.last_n = n;
+        st.since = 0;
+        st.pending = false;                     // (a pending probe was the old workload's)
     }
-    if (e != hipSuccess) { set_err("zp_parse_kernel launch", e); return -2; }
-    return slots ? zp__rec_expand_launch(records, n, (hipStream_t)stream) : 0;
+    if (st.pending) {
+        const hipError_t q = hipEventQuery(st.ev);
+        if (q == hipSuccess) {
+            st.decision = __atomic_load_n(st.word, __ATOMIC_ACQUIRE) == st.token;
+            st.pending = false;
+        } else {
+            (void)hipGetLastError();                          // (hipErrorNotReady)
+        }
+    }
+    if (st.pending || st.since++ % ZP_SLOT_PROBE_EVERY != 0 || !slot_state_init(st))
+        return launch(st.decision, nullptr, 0);
+    // a probe: its expansion writes this token when it finds code tiles (an
+    // earlier probe still in flight writes its own)
+    st.token = st.token + 1 ? st.token + 1 : 1;
+    const int rc = launch(true, st.word_d, st.token);
+    if (rc == 0 && hipEventRecord(st.ev, st_h) == hipSuccess) st.pending = true;
+    else (void)hipGetLastError();
+    return rc;
 }
 
 extern "C" int zp_parse_batch_columns_device(const uint8_t* arena, const uint64_t* offs,

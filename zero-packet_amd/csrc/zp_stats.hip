@@ -277,7 +277,8 @@ extern "C" int zp_probe_tiles_device(const uint8_t* p, uint64_t bytes, uint64_t 
 // The same pattern with record codes (zp_set_record_slots): a full tile
 // stores one byte per frame (a valid code) instead of its 8-B records, and
 // the parse's expansion kernel rewrites the records after it.
-extern "C" int zp__rec_expand_launch(zp_record* records, uint64_t n, hipStream_t stream);
+extern "C" int zp__rec_expand_launch(zp_record* records, uint64_t n, hipStream_t stream, uint32_t* hint,
+                                     uint32_t token);
 extern "C" int zp_probe_tiles_codes_device(const uint8_t* p, uint64_t bytes, uint64_t n,
                                            const uint64_t* offs, const uint32_t* lens,
                                            zp_record* records, uint32_t* sink, void* stream) {
@@ -301,5 +302,5 @@ extern "C" int zp_probe_tiles_codes_device(const uint8_t* p, uint64_t bytes, uin
         snprintf(zp__errbuf(), 256, "zp_probe_tiles_kernel launch: %s", hipGetErrorString(e));
         return -2;
     }
-    return zp__rec_expand_launch(records, n, (hipStream_t)stream);
+    return zp__rec_expand_launch(records, n, (hipStream_t)stream, nullptr, 0);
 }
