@@ -1122,9 +1122,12 @@ __global__ void __launch_bounds__(256) zp_rec_expand_kernel(zp_record* __restric
                             ? ((const uint8_t*)(records + (t0 + lane) * 64))[3] : 0u;
     const uint64_t m = __ballot(b3 >= ZP_CODE_BASE);
     if (!m) return;
-    // (a probe of the automatic mode: every 64th workgroup that finds code
-    // tiles says so, in mapped host memory)
-    if (hint && lane == 0 && (threadIdx.x >> 6) == 0 && (blockIdx.x & 63u) == 0)
+    // (a probe of the automatic mode: the first wave of every 64th
+    // workgroup says, in mapped host memory, when at least 3/4 of its tiles
+    // are code tiles: traffic with a few scattered code tiles, as config 5
+    // has, stays on the one-kernel path)
+    if (hint && lane == 0 && (threadIdx.x >> 6) == 0 && (blockIdx.x & 63u) == 0 &&
+        __builtin_popcountll(m) * 4 >= 3 * ZP_EXPAND_TILES)
         __hip_atomic_store(hint, token, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     uint32_t c[ZP_EXPAND_TILES];
 #pragma unroll
@@ -1161,7 +1164,7 @@ extern "C" int zp_set_record_slots(int mode) {
 // The automatic mode learns per device whether the traffic has code tiles:
 // the first automatic call and every ZP_SLOT_PROBE_EVERY-th one after its
 // predecessor's result is known run the code kernels with a mapped host
-// word the expansion sets when it finds code tiles; once that call has
+// word the expansion sets when sampled waves find mostly code tiles; once that call has
 // completed (an event, queried without waiting) the following calls take
 // the code kernels only if it found some. Traffic without code tiles (c5,
 // c4) then runs zp_parse_kernel alone but for the probes. Under stream
