@@ -187,3 +187,32 @@ def test_slots_mixed_tiles(zp, slots):
     want = check(zp, out, arena, offs, lens)
     inner = (want["flags"] & zp.records.F_IP_IN_IP) != 0
     assert inner.sum() > 1000 and (want["err"] != 0).sum() == 100
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", ["c3", "c5"])
+def test_slots_auto_mode_under_graph_capture(zp, slots, cfg):
+    """The automatic mode inside a HIP graph capture takes its last decision
+    without probing (no event, no host word): the captured launches (the
+    code kernels for c3 after a probe has run, the one-kernel path for c5)
+    replay to the code-free path's records."""
+    n = 4 << 20
+    arena, offs, lens = zp.batch.generate(cfg, n, first=3, device=dev())
+    slots(2)
+    want = torch.empty((n, 8), dtype=torch.uint8, device=arena.device)
+    zp.batch.parse_batch(arena, offs, lens, want, check=False)
+    slots(0)
+    warm = torch.empty((n, 8), dtype=torch.uint8, device=arena.device)
+    for _ in range(3):                            # a probe, completed
+        zp.batch.parse_batch(arena, offs, lens, warm, check=False)
+        torch.cuda.synchronize()
+    rec = torch.empty((n, 8), dtype=torch.uint8, device=arena.device)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        zp.batch.parse_batch(arena, offs, lens, rec, check=False)
+    for fill in (0x00, 0xFF):
+        rec.fill_(fill)
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(rec, want)
+    assert torch.equal(warm, want)
