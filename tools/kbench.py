@@ -57,6 +57,12 @@ def main():
             base_v, m = v.split("@")
             l = libs["base"] if base_v == "base" else ctypes.CDLL(
                 os.path.join(ROOT, "tools", "variants", f"libzp_{base_v}.so"))
+            # (every entry point called with pointers needs its argtypes: a
+            # ctypes default int argument truncates a pointer to 32 bits)
+            l.zp_parse_batch_device.restype = ctypes.c_int
+            l.zp_parse_batch_device.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_uint64] + \
+                [ctypes.c_void_p] * 3
+            l.zp_set_record_slots.restype = ctypes.c_int
             l.zp_set_record_slots.argtypes = [ctypes.c_int]
             libs[v] = l
             slot_mode[v] = int(m)
