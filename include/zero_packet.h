@@ -320,6 +320,10 @@ int zp_parse_batch_device(const uint8_t* arena, const uint64_t* offs,
  * unknown mode.
  */
 int zp_set_record_slots(int mode);
+/* The automatic mode's current decision on the calling thread's device for
+ * batches of at least 2,097,152 frames (1: record codes, 0: one kernel);
+ * the latest completed probe's verdict, 1 before any. For reports. */
+int zp_record_slots_state(void);
 
 /* Host-buffer convenience path: the frames, descriptors and outputs live in
  * host memory (a NIC ring / raw socket buffer). Stages through pinned buffers

@@ -39,6 +39,7 @@ def hip():
         _sig(lib, "zp_last_error", ctypes.c_char_p, [])
         _sig(lib, "zp_parse_batch_device", i32, [vp, vp, vp, u64, vp, vp, vp])
         _sig(lib, "zp_set_record_slots", i32, [i32])
+        _sig(lib, "zp_record_slots_state", i32, [])
         _sig(lib, "zp_ctx_create", vp, [i32, u64])
         _sig(lib, "zp_ctx_destroy", None, [vp])
         _sig(lib, "zp_parse_batch_host", i32, [vp, vp, u64, vp, vp, u64, vp, vp])

@@ -33,11 +33,14 @@ RECORD_CODES_MIN_FRAMES = 1 << 21
 
 def record_codes(n):
     """Whether a parse of n frames takes the record-code kernels under the
-    process' zp_set_record_slots mode (0 auto, 1 always, 2 never)."""
+    process' zp_set_record_slots mode (0 auto, 1 always, 2 never) and, in
+    the automatic mode, the current device's latest probe verdict."""
     lib = _lib.hip()
     mode = lib.zp_set_record_slots(0)
     lib.zp_set_record_slots(mode)
-    return mode == 1 or (mode == 0 and n >= RECORD_CODES_MIN_FRAMES)
+    if mode == 0 and n >= RECORD_CODES_MIN_FRAMES:
+        return lib.zp_record_slots_state() == 1
+    return mode == 1
 SEED = 0x5EED2025
 
 

@@ -1184,6 +1184,16 @@ struct SlotState {
 };
 static SlotState g_slot_state[64];
 
+// The automatic mode's decision on the current device (1: the code kernels,
+// 0: the one-kernel path), for reports.
+extern "C" int zp_record_slots_state(void) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) { (void)hipGetLastError(); dev = 0; }
+    SlotState& st = g_slot_state[dev & 63];
+    std::lock_guard<std::mutex> guard(st.mu);
+    return st.decision ? 1 : 0;
+}
+
 static bool slot_state_init(SlotState& st) {
     if (st.word || st.broken) return !st.broken;
     void* w = nullptr;
