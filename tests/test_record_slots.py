@@ -216,3 +216,47 @@ def test_slots_auto_mode_under_graph_capture(zp, slots, cfg):
         torch.cuda.synchronize()
         assert torch.equal(rec, want)
     assert torch.equal(warm, want)
+
+
+@pytest.mark.gpu
+def test_slots_auto_mode_threads(zp, slots):
+    """zp_parse_batch_device in the automatic mode from four threads at once,
+    each on its own stream with c3 (codes) and c5 (no codes) batches of 2M
+    frames in turn: the per-device decision state is shared, the records
+    are each batch's code-free records."""
+    import threading
+    n = 1 << 21
+    d = dev()
+    data = {cfg: zp.batch.generate(cfg, n, first=11, device=d) for cfg in ("c3", "c5")}
+    slots(2)
+    want = {}
+    for cfg, (a, o, l_) in data.items():
+        r = torch.empty((n, 8), dtype=torch.uint8, device=d)
+        zp.batch.parse_batch(a, o, l_, r, check=False)
+        want[cfg] = r
+    torch.cuda.synchronize()
+    slots(0)
+    errors = []
+
+    def work(k):
+        try:
+            s = torch.cuda.Stream(device=d)
+            rec = torch.empty((n, 8), dtype=torch.uint8, device=d)
+            with torch.cuda.stream(s):
+                for j in range(8):
+                    cfg = ("c3", "c5")[(j + k) % 2]
+                    a, o, l_ = data[cfg]
+                    rec.fill_(0xA5)
+                    zp.batch.parse_batch(a, o, l_, rec, check=False)
+                    s.synchronize()
+                    if not torch.equal(rec, want[cfg]):
+                        errors.append((k, j, cfg))
+        except Exception as e:                  # noqa: BLE001
+            errors.append((k, repr(e)))
+
+    ts = [threading.Thread(target=work, args=(k,)) for k in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errors, errors
