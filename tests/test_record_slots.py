@@ -29,6 +29,70 @@ def test_slot_mode_switch_cpu(built):
     assert lib.zp_set_record_slots(prev) == 1
 
 
+# The code scheme restated on the host (zp_parse.hip rec_code / code_rec):
+# the CPU tests below check its invariants on the oracle's own records, the
+# GPU tests check that the kernels apply it.
+F_ETH, F_ARP, F_V4, F_V6 = 1 << 0, 1 << 1, 1 << 2, 1 << 3
+F_L4 = (0, 1 << 6, 1 << 7, 1 << 8, 1 << 9)              # none, TCP, UDP, ICMPv4, ICMPv6
+CODE_BASE = 0xC0
+
+
+def code_rec(c):
+    x = c - CODE_BASE
+    ec, l3, l4 = x // 15, x // 5 % 3, x % 5
+    f = F_ETH | (F_ARP, F_V4, F_V6)[l3] | F_L4[l4] | ec << 24
+    return f, (14 + 4 * ec + (20 if l3 == 1 else 40)) if l4 else 0
+
+
+def rec_code(flags, offs):
+    """The code of an ABI record, 0 if it has none (zp_parse.hip rec_code)."""
+    for c in range(CODE_BASE, CODE_BASE + 45):
+        x = c - CODE_BASE
+        if x // 5 % 3 == 0 and x % 5:                  # ARP carries no L4 reader
+            continue
+        if code_rec(c) == (flags, offs):
+            return c
+    return 0
+
+
+def test_code_scheme_bijective():
+    """Every valid code names a distinct record whose byte 3 (err << 2 |
+    Ethernet code) is below the 0xC0 marker, so a code tile can never be
+    mistaken for records and the expansion is exact."""
+    codes = [c for c in range(CODE_BASE, CODE_BASE + 45) if not (c - CODE_BASE) // 5 % 3 == 0
+             or (c - CODE_BASE) % 5 == 0]
+    assert len(codes) == 33                             # 3 Ethernet x (ARP + 2 x 5)
+    recs = [code_rec(c) for c in codes]
+    assert len(set(recs)) == len(codes)
+    for c, (f, o) in zip(codes, recs):
+        assert rec_code(f, o) == c and f >> 24 < 3
+    assert (37 << 2 | 3) < CODE_BASE                    # any raw record's byte 3
+
+
+@pytest.mark.parametrize("cfg", ["c1", "c2", "c3", "c4", "c5", "c6"])
+def test_code_scheme_on_oracle_records(zp, cfg):
+    """On each config's frames (and their truncations, for error records):
+    a raw record's byte 3 stays below the marker, and a record with a code
+    is exactly the record its code expands to, so the two stores agree."""
+    a, o, l_ = zp.batch.generate_host(cfg, 1500, first=91)
+    rng = np.random.default_rng(5)
+    cut = l_.astype(np.int64)
+    pick = rng.random(len(cut)) < 0.3
+    cut[pick] = rng.integers(0, cut[pick] + 1)
+    coded = 0
+    for lens in (l_, cut.astype(np.uint32)):
+        rec, ext = orc.parse_batch(a, o, lens)
+        pk = orc.pack(rec, ext)
+        assert (pk["flags"] >> 24 < CODE_BASE).all()
+        for f, off in zip(pk["flags"].tolist(), pk["offs"].tolist()):
+            c = rec_code(f, off)
+            if c:
+                coded += 1
+                assert code_rec(c) == (f, off)
+    if cfg in ("c1", "c2", "c3"):
+        assert coded >= 1500                            # the common form is common here
+
+
 torch = pytest.importorskip("torch")
 
 
