@@ -491,10 +491,10 @@ class PacketParser:
     """parser.rs:22-32. Fields are None or reader views."""
 
     FIELDS = ("ethernet", "arp", "ipv4", "ipv6", "ip_in_ip", "tcp", "udp", "icmpv4", "icmpv6")
-
-    def __init__(self):
-        for f in self.FIELDS:
-            setattr(self, f, None)
+    # the absent fields: class-level None, so building a parser sets only the
+    # readers present (a per-instance loop over FIELDS cost ~1 us per frame
+    # of PacketParser.parse)
+    ethernet = arp = ipv4 = ipv6 = ip_in_ip = tcp = udp = icmpv4 = icmpv6 = None
 
     @classmethod
     def from_record(cls, frame, rec, ext=None):
@@ -566,24 +566,29 @@ class PacketParser:
         longer frames take the batch path with the GIL released."""
         frame = bytes(frame)
         n = len(frame)
-        rec = (ctypes.c_uint32 * 2)()
-        ext = (ctypes.c_uint8 * (2 * _rec.EXT_BYTES))()
-        lib = _lib.hip()
-        dev = _lib.pyhip().zp_device_current()
+        pyhip = _lib.pyhip()
+        dev = pyhip.zp_device_current()
         if dev < 0:
-            raise RuntimeError("zp_device_current failed: " + lib.zp_last_error().decode())
+            raise RuntimeError("zp_device_current failed: " + _lib.hip().zp_last_error().decode())
         pool = _POOLS.get(dev) or _pool(dev)
         if n <= ONE_MAX:
-            # through the resident server: the GIL stays held (_lib.pyhip)
+            # through the resident server: the GIL stays held (_lib.pyhip);
+            # the record lands in the context's own buffers, read before the
+            # context goes back to the pool
             ctx = pool.take()
             try:
-                rc = _lib.pyhip().zp_parse_one(ctx, frame, n, ctypes.addressof(rec),
-                                               ctypes.addressof(ext))
+                b = pool.bufs.get(ctx) or pool.buffers(ctx)
+                rc = pyhip.zp_parse_one(ctx, frame, n, b[2], b[3])
+                if rc >= 0:
+                    return cls._from_words(frame, b[0][0], b[0][1], b[1])
             finally:
                 pool.give(ctx)
-        else:
-            with pool.big_context() as ctx:
-                rc = lib.zp_parse_one(ctx, frame, n, ctypes.addressof(rec), ctypes.addressof(ext))
+            _lib.check(rc, "zp_parse_one")
+        rec = (ctypes.c_uint32 * 2)()
+        ext = (ctypes.c_uint8 * (2 * _rec.EXT_BYTES))()
+        with pool.big_context() as ctx:
+            rc = _lib.hip().zp_parse_one(ctx, frame, n, ctypes.addressof(rec),
+                                         ctypes.addressof(ext))
         if rc < 0:
             _lib.check(rc, "zp_parse_one")
         return cls._from_words(frame, rec[0], rec[1], ext)
@@ -653,6 +658,16 @@ class _DevicePool:
         self.waiting = 0
         self.big = None
         self.big_lock = threading.Lock()
+        self.bufs = {}                          # pooled context -> its record / ext buffers
+
+    def buffers(self, ctx):
+        """The record and ext buffers of pooled context `ctx` (and their
+        addresses), made on its first call; only the caller holding ctx
+        touches them."""
+        rec = (ctypes.c_uint32 * 2)()
+        ext = (ctypes.c_uint8 * (2 * _rec.EXT_BYTES))()
+        b = self.bufs[ctx] = (rec, ext, ctypes.addressof(rec), ctypes.addressof(ext))
+        return b
 
     def _create(self, chunk):
         lib = _lib.hip()
