@@ -22,6 +22,7 @@ class FakeLib:
         self.lock = threading.Lock()
         self.busy = set()
         self.overlap = 0
+        self.bufs = {}             # context -> the (record, ext) addresses it was given
 
     def zp_device_current(self):
         return self.device
@@ -35,6 +36,8 @@ class FakeLib:
     def zp_parse_one(self, ctx, frame, n, rec, ext):
         with self.lock:
             assert ctx not in self.busy, "a context served two calls at once"
+            if n <= 64 << 10:      # pooled contexts (the large one gets a call's own)
+                assert self.bufs.setdefault(ctx, (rec, ext)) == (rec, ext), "buffers moved"
             self.busy.add(ctx)
             self.overlap = max(self.overlap, len(self.busy))
         time.sleep(0.002)
@@ -87,6 +90,8 @@ def test_threads_run_concurrently_on_own_contexts(zp, fake):
     assert len(fake.created) <= 8
     pool = P._POOLS[0]
     assert sorted(pool.free) == sorted(pool.all)   # every lease returned
+    # each context writes into record buffers of its own, kept across calls
+    assert len(set(fake.bufs.values())) == len(fake.bufs) == len(pool.all)
 
 
 def test_pool_bound_waits(zp, fake, monkeypatch):
